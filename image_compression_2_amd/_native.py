@@ -1,0 +1,147 @@
+"""ctypes binding of libic2ops.so (the C ABI declared in include/ic2ops.h).
+
+The product path has NO CPU fallback: every public op requires ROCm tensors and the in-tree
+HIP library; anything else raises.  (The CPU restatement in ``oracle/`` is test infrastructure.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libic2ops.so")
+
+F32, BF16 = 0, 1
+ACT_LINEAR, ACT_LRELU = 0, 1
+NHWC, NCHW = 0, 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS = {
+    "ic2_abi_version": [],
+    "ic2_quantize_uniform": [_P, _I64, _I, _P, _P, _P],
+    "ic2_quantize_codebook_argmin": [_P, _I64, _P, _I, _P, _P, _P, _P],
+    "ic2_codebook_lookup": [_P, _I64, _P, _I, _P, _P, _P],
+    "ic2_gumbel_softmax_quantize": [_P, _I64, _P, _I, _P, _F, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
+                                    _P],
+    "ic2_bias_act": [_P, _P, _P, _I, _I64, _I64, _I64, _I, _F, _F, _F, _P],
+    "ic2_upfirdn2d": [_P, _P, _I, _I64, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P],
+    "ic2_filtered_lrelu": [_P, _P, _I, _I64, _I64, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _F,
+                           _F, _I, _P],
+    "ic2_flrelu_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F,
+                        _I, _P, _P],
+    "ic2_fc": [_P, _I64, _P, _P, _P, _I, _I, _I, _F, _F, _I, _F, _F, _P],
+    "ic2_pack_weight": [_P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _I, _P, _P],
+    "ic2_modconv_prep": [_P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P],
+    "ic2_conv_igemm": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I,
+                       _P],
+    "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
+    "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "ic2_nhwc_to_nchw": [_P, _I, _P, _I, _I, _I, _I, _I, _P],
+    "ic2_group_norm_stats_floats": [_I, _I, _I],
+    "ic2_group_norm_stats": [_P, _I, _I, _I, _I, _I, _I, _F, _P, _P],
+    "ic2_gn_lrelu_pool": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P],
+    "ic2_global_avg_pool_floats": [_I, _I, _I, _I],
+    "ic2_global_avg_pool": [_P, _I, _I, _I, _I, _I, _P, _P],
+    "ic2_reparameterize": [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
+    "ic2_uint8_sse": [_P, _P, _I64, _I64, _P, _P],
+    "ic2_resize_bilinear": [_P, _P, _I64, _I, _I, _I, _I, _P],
+}
+_RESTYPE = {"ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def load():
+    """Load libic2ops.so (built in-tree by ``build_native``).  Raises if missing -- no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"{LIB_PATH} is missing: build it with `python -m image_compression_2_amd.build_native` "
+                "(there is no CPU fallback for the product path)")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.ic2_last_error.restype = ctypes.c_char_p
+        lib.ic2_last_error.argtypes = []
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, _I)
+        _lib = lib
+    return _lib
+
+
+def exported_symbols():
+    return ["ic2_last_error"] + list(_SIGS)
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ic2_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+# ------------------------------------------------------------------------------------------------
+# tensor helpers
+# ------------------------------------------------------------------------------------------------
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("image_compression_2_amd runs on ROCm devices only (got a CPU tensor); "
+                               "the CPU restatement lives in oracle/ and is test infrastructure")
+        if not t.is_contiguous():
+            raise RuntimeError("expected a contiguous tensor")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t=None):
+    dev = t.device if t is not None else None
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {dt}")
+
+
+def torch_dtype(precision):
+    if precision in ("fp32", "f32", torch.float32):
+        return torch.float32
+    if precision in ("bf16", torch.bfloat16):
+        return torch.bfloat16
+    raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+
+
+def pad32(c):
+    return (int(c) + 31) // 32 * 32

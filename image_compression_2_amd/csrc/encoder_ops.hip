@@ -1,0 +1,389 @@
+// HVAE_VGG_Encoder support kernels (/root/reference/stylegan3_hvae_full.py:105-247) and the metric /
+// resize helpers of the compressor API.  All HBM-bound; NHWC with padded channel stride c_p.
+#include "common.h"
+
+namespace ic2 {
+
+static int grid_1d(int64_t total, int per = 1) {
+  int64_t g = ceil_div(ceil_div(total, per), 256);
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
+  return (int)g;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int n,
+                                                           int c, int hw, int c_p, const float* __restrict__ scale) {
+  const int64_t total = (int64_t)n * hw * c_p;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(e % c_p);
+    const int64_t pix = e / c_p;
+    const int p = (int)(pix % hw);
+    const int64_t nn = pix / hw;
+    float v = ch < c ? x[(nn * c + ch) * hw + p] : 0.f;
+    if (scale) v *= scale[nn * c_p + ch];
+    st(y + e, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_to_nchw_kernel(const T* __restrict__ x, float* __restrict__ y, int n, int c,
+                                                           int hw, int c_p) {
+  const int64_t total = (int64_t)n * c * hw;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int p = (int)(e % hw);
+    const int64_t r = e / hw;
+    const int ch = (int)(r % c);
+    const int64_t nn = r / c;
+    y[e] = ld(x + (nn * hw + p) * c_p + ch);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// GroupNorm statistics: stage 1 = per (n, pixel chunk) per-group partial sums (f64) written to
+// `part`; stage 2 = per (n, group) ordered sum over chunks -> mean, rstd.  Deterministic.
+// ------------------------------------------------------------------------------------------------
+constexpr int GN_CHUNK_PIX = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y, int hw, int c_p, int c, int groups,
+                                                         int nchunks, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double sred[];  // [2][256]
+  const int chunk = blockIdx.x % nchunks;
+  const int nn = blockIdx.x / nchunks;
+  const int cpg = c / groups;
+  const int p0 = chunk * GN_CHUNK_PIX;
+  const int p1 = min(hw, p0 + GN_CHUNK_PIX);
+  const T* yb = y + (int64_t)nn * hw * c_p;
+  double* sum = sred;
+  double* sq = sred + 256;
+  for (int g = 0; g < groups; ++g) {
+    // elements of group g in this chunk: (p1 - p0) * cpg, channel fastest
+    const int cnt = (p1 - p0) * cpg;
+    float s = 0.f, q = 0.f;
+    for (int e = threadIdx.x; e < cnt; e += 256) {
+      const int p = p0 + e / cpg;
+      const int ch = g * cpg + e % cpg;
+      const float v = ld(yb + (int64_t)p * c_p + ch);
+      s += v;
+      q += v * v;
+    }
+    sum[threadIdx.x] = s;
+    sq[threadIdx.x] = q;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (threadIdx.x < off) {
+        sum[threadIdx.x] += sum[threadIdx.x + off];
+        sq[threadIdx.x] += sq[threadIdx.x + off];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      double* o = part + (((int64_t)nn * groups + g) * nchunks + chunk) * 2;
+      o[0] = sum[0];
+      o[1] = sq[0];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const double* __restrict__ part, int ngroups_total,
+                                                          int nchunks, double count, float eps,
+                                                          float* __restrict__ stats) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ngroups_total) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    s += part[((int64_t)i * nchunks + k) * 2 + 0];
+    q += part[((int64_t)i * nchunks + k) * 2 + 1];
+  }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0) var = 0;
+  stats[i * 2 + 0] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// ------------------------------------------------------------------------------------------------
+// GroupNorm apply + lrelu (+ 2x2 average pool); 4 channels per thread
+// ------------------------------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y, TO* __restrict__ out, int n, int h,
+                                                       int w, int c_p, int c, int groups,
+                                                       const float* __restrict__ stats,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float slope, int pool) {
+  const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
+  const int cq = c_p / 4;
+  const int64_t total = (int64_t)n * oh * ow * cq;
+  const int cpg = c / groups;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ch0 = (int)(e % cq) * 4;
+    const int64_t pix = e / cq;
+    const int ox = (int)(pix % ow);
+    const int oy = (int)((pix / ow) % oh);
+    const int nn = (int)(pix / ((int64_t)ow * oh));
+    float res[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int ch = ch0 + k;
+      res[k] = 0.f;
+      if (ch >= c) continue;
+      const int g = ch / cpg;
+      const float mean = stats[((int64_t)nn * groups + g) * 2 + 0];
+      const float rstd = stats[((int64_t)nn * groups + g) * 2 + 1];
+      const float ga = gamma[ch], be = beta[ch];
+      auto f = [&](int yy, int xx) {
+        const float v = ld(y + (((int64_t)nn * h + yy) * w + xx) * c_p + ch);
+        const float t = (v - mean) * rstd * ga + be;
+        return t < 0.f ? t * slope : t;
+      };
+      if (pool) {
+        const float a0 = f(2 * oy, 2 * ox), a1 = f(2 * oy, 2 * ox + 1);
+        const float a2 = f(2 * oy + 1, 2 * ox), a3 = f(2 * oy + 1, 2 * ox + 1);
+        res[k] = (((a0 + a1) + a2) + a3) / 4.f;
+      } else {
+        res[k] = f(oy, ox);
+      }
+    }
+    TO* o = out + pix * c_p + ch0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st(o + k, res[k]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// global average pool: stage 1 per (n, chunk) channel partials, stage 2 ordered chunk sum
+// ------------------------------------------------------------------------------------------------
+constexpr int GAP_CHUNK = 64;
+
+template <typename T>
+__global__ void __launch_bounds__(256) gap_partial_kernel(const T* __restrict__ x, int hw, int c_p, int nchunks,
+                                                          float* __restrict__ part) {
+  const int chunk = blockIdx.y;
+  const int nn = blockIdx.z;
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch >= c_p) return;
+  const int p0 = chunk * GAP_CHUNK, p1 = min(hw, p0 + GAP_CHUNK);
+  float s = 0.f;
+  for (int p = p0; p < p1; ++p) s += ld(x + ((int64_t)nn * hw + p) * c_p + ch);
+  part[((int64_t)nn * nchunks + chunk) * c_p + ch] = s;
+}
+
+__global__ void __launch_bounds__(256) gap_finalize_kernel(const float* __restrict__ part, int n, int c_p, int c,
+                                                           int nchunks, int hw, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)n * c) return;
+  const int ch = (int)(i % c);
+  const int64_t nn = i / c;
+  float s = 0.f;
+  for (int k = 0; k < nchunks; ++k) s += part[(nn * nchunks + k) * c_p + ch];
+  out[i] = s / (float)hw;
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) reparam_kernel(const float* __restrict__ params, const float* __restrict__ eps,
+                                                      int n, int num_ws, int w_dim, int ws_total, int ws_off,
+                                                      float* __restrict__ w_out, float* __restrict__ mean_out,
+                                                      float* __restrict__ logvar_out) {
+  const int64_t total = (int64_t)n * num_ws * w_dim;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d = (int)(e % w_dim);
+    const int64_t r = e / w_dim;
+    const int s = (int)(r % num_ws);
+    const int64_t nn = r / num_ws;
+    const float m = params[r * 2 * w_dim + d];
+    const float lv = params[r * 2 * w_dim + w_dim + d];
+    const int64_t o = (nn * ws_total + ws_off + s) * w_dim + d;
+    if (mean_out) mean_out[o] = m;
+    if (logvar_out) logvar_out[o] = lv;
+    if (w_out) {
+      const float sd = expf(0.5f * lv);
+      w_out[o] = eps ? m + eps[e] * sd : m;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int to_u8(float v) {
+  float t = v * 0.5f + 0.5f;
+  t = fminf(fmaxf(t, 0.f), 1.f);
+  return (int)(t * 255.f);  // truncation, as numpy astype(np.uint8) on [0, 255]
+}
+
+__global__ void __launch_bounds__(256) uint8_sse_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                        int64_t per_img, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int64_t base = (int64_t)blockIdx.x * per_img;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < per_img; i += 256) {
+    const int d = to_u8(a[base + i]) - to_u8(b[base + i]);
+    acc += (double)(d * d);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// F.interpolate(bilinear, align_corners=False): src = max(0, (dst + 0.5) * in/out - 0.5)
+__global__ void __launch_bounds__(256) resize_bilinear_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                              int64_t nc, int h, int w, int oh, int ow) {
+  const int64_t total = nc * oh * ow;
+  const float sh = (float)h / (float)oh, sw = (float)w / (float)ow;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ox = (int)(e % ow);
+    const int oy = (int)((e / ow) % oh);
+    const int64_t pl = e / ((int64_t)ow * oh);
+    float sy = fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
+    float sx = fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly = sy - y0, lx = sx - x0;
+    const float* p = x + pl * h * w;
+    const float v = (1.f - ly) * ((1.f - lx) * p[y0 * w + x0] + lx * p[y0 * w + x1]) +
+                    ly * ((1.f - lx) * p[y1 * w + x0] + lx * p[y1 * w + x1]);
+    y[e] = v;
+  }
+}
+
+}  // namespace ic2
+
+using namespace ic2;
+
+extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c, int h, int w, int c_p,
+                                const float* scale, void* stream) {
+  IC2_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && c_p >= c, "nchw_to_nhwc: bad arguments");
+  const int64_t total = (int64_t)n * h * w * c_p;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, x, (float*)y, n, c, h * w, c_p,
+                       scale);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, x, (bf16_t*)y, n, c, h * w,
+                       c_p, scale);
+  else
+    IC2_CHECK_ARG(false, "nchw_to_nhwc: bad dtype");
+  IC2_CHECK_LAUNCH("nchw_to_nhwc");
+  return IC2_OK;
+}
+
+extern "C" int ic2_nhwc_to_nchw(const void* x, int dtype, float* y, int n, int c, int h, int w, int c_p, void* stream) {
+  IC2_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && c_p >= c, "nhwc_to_nchw: bad arguments");
+  const int64_t total = (int64_t)n * h * w * c;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, (const float*)x, y, n, c, h * w,
+                       c_p);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, (const bf16_t*)x, y, n, c,
+                       h * w, c_p);
+  else
+    IC2_CHECK_ARG(false, "nhwc_to_nchw: bad dtype");
+  IC2_CHECK_LAUNCH("nhwc_to_nchw");
+  return IC2_OK;
+}
+
+extern "C" int64_t ic2_group_norm_stats_floats(int n, int hw, int groups) {
+  const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
+  return stats_floats + (int64_t)n * groups * ceil_div(hw, GN_CHUNK_PIX) * 2 * 2;
+}
+
+extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c, int groups, float eps,
+                                    float* stats_out, void* stream) {
+  IC2_CHECK_ARG(y && stats_out && n > 0 && hw > 0 && c > 0 && groups > 0 && c % groups == 0 && c_p >= c,
+                "group_norm_stats: bad arguments");
+  const int nchunks = (int)ceil_div(hw, GN_CHUNK_PIX);
+  // partials live right after the stats (8-byte aligned)
+  const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
+  double* part = reinterpret_cast<double*>(stats_out + stats_floats);
+  hipStream_t s = as_stream(stream);
+  const size_t lds = 2 * 256 * sizeof(double);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(n * nchunks), dim3(256), lds, s, (const float*)y, hw, c_p, c,
+                       groups, nchunks, part);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(n * nchunks), dim3(256), lds, s, (const bf16_t*)y, hw, c_p, c,
+                       groups, nchunks, part);
+  else
+    IC2_CHECK_ARG(false, "group_norm_stats: bad dtype");
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)ceil_div(n * groups, 256)), dim3(256), 0, s, part, n * groups,
+                     nchunks, (double)hw * (c / groups), eps, stats_out);
+  IC2_CHECK_LAUNCH("group_norm_stats");
+  return IC2_OK;
+}
+
+extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p,
+                                 int c, int groups, const float* stats, const float* gamma, const float* beta,
+                                 float slope, int pool, void* stream) {
+  IC2_CHECK_ARG(y && out && stats && gamma && beta && n > 0 && h > 0 && w > 0 && c_p % 4 == 0 && c <= c_p,
+                "gn_lrelu_pool: bad arguments");
+  IC2_CHECK_ARG(!pool || (h >= 2 && w >= 2), "gn_lrelu_pool: pooling needs H, W >= 2");
+  const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
+  const int64_t total = (int64_t)n * oh * ow * (c_p / 4);
+  hipStream_t s = as_stream(stream);
+#define IC2_GN_LAUNCH(TI, TO)                                                                                     \
+  hipLaunchKernelGGL((gn_apply_kernel<TI, TO>), dim3(grid_1d(total)), dim3(256), 0, s, (const TI*)y, (TO*)out, n, h, \
+                     w, c_p, c, groups, stats, gamma, beta, slope, pool)
+  if (dtype_in == IC2_F32 && dtype_out == IC2_F32) IC2_GN_LAUNCH(float, float);
+  else if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(bf16_t, bf16_t);
+  else if (dtype_in == IC2_BF16 && dtype_out == IC2_F32) IC2_GN_LAUNCH(bf16_t, float);
+  else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(float, bf16_t);
+  else IC2_CHECK_ARG(false, "gn_lrelu_pool: bad dtypes");
+#undef IC2_GN_LAUNCH
+  IC2_CHECK_LAUNCH("gn_lrelu_pool");
+  return IC2_OK;
+}
+
+extern "C" int64_t ic2_global_avg_pool_floats(int n, int hw, int c_p, int c) {
+  return (int64_t)n * c + (int64_t)n * ceil_div(hw, GAP_CHUNK) * c_p;
+}
+
+extern "C" int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int c_p, int c, float* out, void* stream) {
+  IC2_CHECK_ARG(x && out && n > 0 && hw > 0 && c > 0 && c_p >= c, "global_avg_pool: bad arguments");
+  const int nchunks = (int)ceil_div(hw, GAP_CHUNK);
+  float* part = out + (int64_t)n * c;
+  hipStream_t s = as_stream(stream);
+  dim3 grid((unsigned)ceil_div(c_p, 256), nchunks, n);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(gap_partial_kernel<float>, grid, dim3(256), 0, s, (const float*)x, hw, c_p, nchunks, part);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(gap_partial_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, hw, c_p, nchunks, part);
+  else
+    IC2_CHECK_ARG(false, "global_avg_pool: bad dtype");
+  hipLaunchKernelGGL(gap_finalize_kernel, dim3((unsigned)ceil_div((int64_t)n * c, 256)), dim3(256), 0, s, part, n, c_p,
+                     c, nchunks, hw, out);
+  IC2_CHECK_LAUNCH("global_avg_pool");
+  return IC2_OK;
+}
+
+extern "C" int ic2_reparameterize(const float* params, const float* eps, int n, int num_ws, int w_dim, int ws_total,
+                                  int ws_off, float* w_out, float* mean_out, float* logvar_out, void* stream) {
+  IC2_CHECK_ARG(params && n > 0 && num_ws > 0 && w_dim > 0 && ws_off >= 0 && ws_off + num_ws <= ws_total,
+                "reparameterize: bad arguments");
+  const int64_t total = (int64_t)n * num_ws * w_dim;
+  hipLaunchKernelGGL(reparam_kernel, dim3(grid_1d(total)), dim3(256), 0, as_stream(stream), params, eps, n, num_ws,
+                     w_dim, ws_total, ws_off, w_out, mean_out, logvar_out);
+  IC2_CHECK_LAUNCH("reparameterize");
+  return IC2_OK;
+}
+
+extern "C" int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img, double* sse_out,
+                             void* stream) {
+  IC2_CHECK_ARG(a && b && sse_out && n_img > 0 && per_img > 0 && n_img < (1LL << 31), "uint8_sse: bad arguments");
+  hipLaunchKernelGGL(uint8_sse_kernel, dim3((unsigned)n_img), dim3(256), 0, as_stream(stream), a, b, per_img, sse_out);
+  IC2_CHECK_LAUNCH("uint8_sse");
+  return IC2_OK;
+}
+
+extern "C" int ic2_resize_bilinear(const float* x, float* y, int64_t nc, int h, int w, int oh, int ow, void* stream) {
+  IC2_CHECK_ARG(x && y && nc > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "resize_bilinear: bad arguments");
+  hipLaunchKernelGGL(resize_bilinear_kernel, dim3(grid_1d(nc * oh * ow)), dim3(256), 0, as_stream(stream), x, y, nc, h,
+                     w, oh, ow);
+  IC2_CHECK_LAUNCH("resize_bilinear");
+  return IC2_OK;
+}

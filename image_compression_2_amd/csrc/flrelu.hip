@@ -1,0 +1,330 @@
+// Fused filtered leaky-ReLU [SG3-public: torch_utils/ops/filtered_lrelu.py, whose reference path is
+//   bias_act(b) -> upfirdn2d(fu, up, padding, gain=up^2) -> bias_act(lrelu, slope, gain, clamp)
+//   -> upfirdn2d(fd, down)]; called by SynthesisLayer.forward for every layer of
+// G.synthesis (/root/reference/stylegan3_hvae_full.py:274,329).
+//
+// One workgroup = one (sample, 16x8 output tile, 16-channel block).  Lanes own channel PAIRS
+// (packed fp32 math, bf16x2 loads), the spatial FIR runs from registers with every tap index
+// resolved at compile time (polyphase: zero-inserted samples are never multiplied), and the
+// up-sampled grid lives only in LDS:
+//   stage 1  vertical up-FIR   : input column (registers)        -> LDS  a_v[RAY][NINX]
+//   stage 2  horizontal up-FIR : LDS row -> lrelu*gain, clamp -> horizontal down-FIR (registers)
+//                                -> written back over the thread's own LDS row (no barrier)
+//   stage 3  vertical down-FIR : LDS column -> * post_scale -> global
+// Filters are separable 1-D taps (the StyleGAN3-T configuration).  Zero padding / negative
+// padding (crop) is exact: input samples outside [0, L) are zero, as in the reference.
+#include "common.h"
+
+namespace ic2 {
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct FlrArgs {
+  const void* x;
+  void* y;
+  const float* bias;
+  const float* post_scale;  // [n][c_p] or null
+  int64_t xsn, xsy, xsx, xsc;  // input strides (elements)
+  int64_t ysn, ysy, ysx, ysc;  // output strides
+  int c, c_p;                   // valid channels, post_scale row stride
+  int in_h, in_w, out_h, out_w;
+  int py0, px0;                 // leading padding
+  int tiles_x, tiles_y, cblocks;
+  float gain, slope, clamp;
+  float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
+  float gd[12];  // flipped (unless flip_filter)
+};
+
+template <int U, int D, int TU, int TD, int TOY, int TOX>
+struct FlrGeom {
+  static constexpr int RAY = (TOY - 1) * D + TD;       // lrelu-grid rows of one tile
+  static constexpr int RAX = (TOX - 1) * D + TD;
+  static constexpr int NINY = (RAY + TU - 2) / U + 1;  // input rows feeding them
+  static constexpr int NINX = (RAX + TU - 2) / U + 1;
+  static constexpr int NINXP = NINX | 1;               // odd row pitch: conflict-free ds_read_b64
+};
+
+template <typename T> __device__ __forceinline__ f2v load2(const T* p, int64_t sc, bool pair, bool second_ok);
+template <> __device__ __forceinline__ f2v load2<float>(const float* p, int64_t sc, bool pair, bool ok2) {
+  if (pair) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    return f2v{v.x, v.y};
+  }
+  return f2v{p[0], ok2 ? p[sc] : 0.f};
+}
+template <> __device__ __forceinline__ f2v load2<bf16_t>(const bf16_t* p, int64_t sc, bool pair, bool ok2) {
+  if (pair) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+    return f2v{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+  }
+  return f2v{bf2f(p[0]), ok2 ? bf2f(p[sc]) : 0.f};
+}
+template <typename T> __device__ __forceinline__ void store2(T* p, int64_t sc, bool pair, bool ok2, f2v v);
+template <> __device__ __forceinline__ void store2<float>(float* p, int64_t sc, bool pair, bool ok2, f2v v) {
+  if (pair) {
+    *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y);
+  } else {
+    p[0] = v.x;
+    if (ok2) p[sc] = v.y;
+  }
+}
+template <> __device__ __forceinline__ void store2<bf16_t>(bf16_t* p, int64_t sc, bool pair, bool ok2, f2v v) {
+  if (pair) {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  } else {
+    p[0] = f2bf(v.x);
+    if (ok2) p[sc] = f2bf(v.y);
+  }
+}
+
+__device__ __forceinline__ f2v act2(f2v a, float slope, float gain, float clamp) {
+  f2v r;
+  r.x = lrelu_gain_clamp(a.x, slope, gain, clamp);
+  r.y = lrelu_gain_clamp(a.y, slope, gain, clamp);
+  return r;
+}
+
+constexpr int FLR_THREADS = 128;
+constexpr int FLR_CPB = 16;              // channels per workgroup
+constexpr int FLR_NCG = FLR_CPB / 2;     // channel pairs
+
+template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DELTA, int TOY, int TOX>
+__global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
+  using G = FlrGeom<U, D, TU, TD, TOY, TOX>;
+  constexpr int RAY = G::RAY, RAX = G::RAX, NINY = G::NINY, NINX = G::NINX, NINXP = G::NINXP;
+  constexpr int NCG = FLR_NCG;
+  __shared__ __attribute__((aligned(16))) f2v buf[RAY * NINXP * NCG];
+
+  int bid = blockIdx.x;
+  const int cb = bid % a.cblocks;
+  bid /= a.cblocks;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int n = bid / a.tiles_y;
+
+  const int oy0 = ty * TOY, ox0 = tx * TOX;
+  // first input sample feeding the tile: s_lo = (ka - p0 + DELTA) / U with ka = o0 * D
+  const int sy0 = (oy0 * D - a.py0 + DELTA) / U;
+  const int sx0 = (ox0 * D - a.px0 + DELTA) / U;
+  const int c0 = cb * FLR_CPB;
+
+  const TI* __restrict__ xin = reinterpret_cast<const TI*>(a.x) + (int64_t)n * a.xsn;
+  TO* __restrict__ yout = reinterpret_cast<TO*>(a.y) + (int64_t)n * a.ysn;
+
+  // ---------------- stage 1: vertical up-FIR of NINX input columns
+  for (int item = threadIdx.x; item < NINX * NCG; item += FLR_THREADS) {
+    const int xs = item / NCG;
+    const int cg = item - xs * NCG;
+    const int c = c0 + 2 * cg;
+    const int ix = sx0 + xs;
+    const bool col_ok = (unsigned)ix < (unsigned)a.in_w && c < a.c;
+    const bool ok2 = c + 1 < a.c;
+    f2v bsum = f2v{0.f, 0.f};
+    if (a.bias && col_ok) bsum = f2v{a.bias[c], ok2 ? a.bias[c + 1] : 0.f};
+    f2v in[NINY];
+#pragma unroll
+    for (int j = 0; j < NINY; ++j) {
+      const int iy = sy0 + j;
+      if (col_ok && (unsigned)iy < (unsigned)a.in_h) {
+        const TI* p = xin + (int64_t)iy * a.xsy + (int64_t)ix * a.xsx + (int64_t)c * a.xsc;
+        in[j] = load2<TI>(p, a.xsc, CHLAST && ok2, ok2) + bsum;
+      } else {
+        in[j] = f2v{0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RAY; ++i) {
+      f2v acc = f2v{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NINY; ++j) {
+        const int t = U * j + DELTA - i;
+        if (t >= 0 && t < TU) acc += a.gu[t] * in[j];
+      }
+      buf[(i * NINXP + xs) * NCG + cg] = acc;
+    }
+  }
+  __syncthreads();
+
+  // ---------------- stage 2: horizontal up-FIR, activation, horizontal down-FIR per grid row
+  for (int item = threadIdx.x; item < RAY * NCG; item += FLR_THREADS) {
+    const int i = item / NCG;
+    const int cg = item - i * NCG;
+    f2v in[NINX];
+#pragma unroll
+    for (int j = 0; j < NINX; ++j) in[j] = buf[(i * NINXP + j) * NCG + cg];
+    f2v d[TOX];
+#pragma unroll
+    for (int o = 0; o < TOX; ++o) d[o] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < RAX; ++k) {
+      f2v v = f2v{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NINX; ++j) {
+        const int t = U * j + DELTA - k;
+        if (t >= 0 && t < TU) v += a.gu[t] * in[j];
+      }
+      v = act2(v, a.slope, a.gain, a.clamp);
+#pragma unroll
+      for (int o = 0; o < TOX; ++o) {
+        const int t = k - o * D;
+        if (t >= 0 && t < TD) d[o] += a.gd[t] * v;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < TOX; ++o) buf[(i * NINXP + o) * NCG + cg] = d[o];
+  }
+  __syncthreads();
+
+  // ---------------- stage 3: vertical down-FIR per output column, store
+  for (int item = threadIdx.x; item < TOX * NCG; item += FLR_THREADS) {
+    const int ox = item / NCG;
+    const int cg = item - ox * NCG;
+    const int c = c0 + 2 * cg;
+    const int gx = ox0 + ox;
+    if (gx >= a.out_w || c >= a.c) continue;
+    const bool ok2 = c + 1 < a.c;
+    f2v o[TOY];
+#pragma unroll
+    for (int r = 0; r < TOY; ++r) o[r] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RAY; ++i) {
+      const f2v v = buf[(i * NINXP + ox) * NCG + cg];
+#pragma unroll
+      for (int r = 0; r < TOY; ++r) {
+        const int t = i - r * D;
+        if (t >= 0 && t < TD) o[r] += a.gd[t] * v;
+      }
+    }
+    f2v ps = f2v{1.f, 1.f};
+    if (a.post_scale) ps = f2v{a.post_scale[(int64_t)n * a.c_p + c], ok2 ? a.post_scale[(int64_t)n * a.c_p + c + 1] : 0.f};
+#pragma unroll
+    for (int r = 0; r < TOY; ++r) {
+      const int gy = oy0 + r;
+      if (gy < a.out_h) {
+        TO* p = yout + (int64_t)gy * a.ysy + (int64_t)gx * a.ysx + (int64_t)c * a.ysc;
+        store2<TO>(p, a.ysc, CHLAST && ok2, ok2, o[r] * ps);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dispatch
+// ------------------------------------------------------------------------------------------------
+constexpr int FLR_TOY = 16, FLR_TOX = 8;
+
+template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD>
+static int launch_delta(const FlrArgs& a, int delta, int grid, hipStream_t s) {
+#define IC2_FLR_CASE(DL)                                                                                         \
+  case DL:                                                                                                       \
+    if constexpr (DL < U) {                                                                                      \
+      hipLaunchKernelGGL((flrelu_kernel<TI, TO, CHLAST, U, D, TU, TD, DL, FLR_TOY, FLR_TOX>), dim3(grid),         \
+                         dim3(FLR_THREADS), 0, s, a);                                                            \
+      return IC2_OK;                                                                                             \
+    }                                                                                                            \
+    break;
+  switch (delta) {
+    IC2_FLR_CASE(0)
+    IC2_FLR_CASE(1)
+    IC2_FLR_CASE(2)
+    IC2_FLR_CASE(3)
+  }
+#undef IC2_FLR_CASE
+  return IC2_E_UNSUPPORTED;
+}
+
+template <typename TI, typename TO, bool CHLAST>
+static int launch_cfg(const FlrArgs& a, int up, int down, int tu, int td, int delta, int grid, hipStream_t s) {
+  if (up == 2 && down == 2 && tu == 12 && td == 12) return launch_delta<TI, TO, CHLAST, 2, 2, 12, 12>(a, delta, grid, s);
+  if (up == 4 && down == 2 && tu == 24 && td == 12) return launch_delta<TI, TO, CHLAST, 4, 2, 24, 12>(a, delta, grid, s);
+  return IC2_E_UNSUPPORTED;
+}
+
+static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bool chlast, int n, int c, int c_p,
+                         int in_h, int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd,
+                         int fd_taps, const float* b, int up, int down, int px0, int px1, int py0, int py1,
+                         float gain, float slope, float clamp, int flip, const float* post_scale, void* stream,
+                         const char* name) {
+  IC2_CHECK_ARG(x && y, "%s: null pointer", name);
+  IC2_CHECK_ARG(n > 0 && c > 0 && in_h > 0 && in_w > 0 && up >= 1 && down >= 1, "%s: bad geometry", name);
+  IC2_CHECK_ARG(fu_taps >= 1 && fd_taps >= 1 && fu_taps <= 24 && fd_taps <= 12, "%s: unsupported taps", name);
+  const int ew = (in_w * up + (px0 + px1) - (fu_taps - 1) - (fd_taps - 1) + (down - 1)) / down;
+  const int eh = (in_h * up + (py0 + py1) - (fu_taps - 1) - (fd_taps - 1) + (down - 1)) / down;
+  IC2_CHECK_ARG(out_h == eh && out_w == ew, "%s: output %dx%d, expected %dx%d", name, out_h, out_w, eh, ew);
+  IC2_CHECK_ARG(out_h > 0 && out_w > 0, "%s: empty output", name);
+  // one polyphase offset serves both axes -> needs px0 == py0 (mod up); the fused instances exist for
+  // the StyleGAN3-T configurations only
+  const int dx = ((px0 % up) + up) % up, dy = ((py0 % up) + up) % up;
+  if (dx != dy) {
+    set_error("%s: px0 and py0 differ mod up", name);
+    return IC2_E_UNSUPPORTED;
+  }
+  FlrArgs a;
+  a.x = x; a.y = y; a.bias = b; a.post_scale = post_scale;
+  if (chlast) {
+    a.xsc = 1; a.xsx = c_p; a.xsy = (int64_t)in_w * c_p; a.xsn = (int64_t)in_h * in_w * c_p;
+    a.ysc = 1; a.ysx = c_p; a.ysy = (int64_t)out_w * c_p; a.ysn = (int64_t)out_h * out_w * c_p;
+  } else {
+    a.xsx = 1; a.xsy = in_w; a.xsc = (int64_t)in_h * in_w; a.xsn = (int64_t)c * in_h * in_w;
+    a.ysx = 1; a.ysy = out_w; a.ysc = (int64_t)out_h * out_w; a.ysn = (int64_t)c * out_h * out_w;
+  }
+  a.c = chlast ? c_p : c;  // NHWC: padded channels are processed too (they are zero) and stay zero
+  a.c_p = c_p;
+  a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w;
+  a.py0 = py0; a.px0 = px0;
+  a.tiles_x = (int)ceil_div(out_w, FLR_TOX);
+  a.tiles_y = (int)ceil_div(out_h, FLR_TOY);
+  a.cblocks = (int)ceil_div(a.c, FLR_CPB);
+  a.gain = gain; a.slope = slope; a.clamp = clamp;
+  for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
+  for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;
+  // NOTE: fu / fd are HOST pointers here (filters are layer constants; they travel in the kernarg)
+  for (int t = 0; t < fu_taps; ++t) a.gu[t] = (fu ? (flip ? fu[t] : fu[fu_taps - 1 - t]) : 1.f) * (float)up;
+  for (int t = 0; t < fd_taps; ++t) a.gd[t] = fd ? (flip ? fd[t] : fd[fd_taps - 1 - t]) : 1.f;
+  const int64_t grid = (int64_t)n * a.tiles_y * a.tiles_x * a.cblocks;
+  IC2_CHECK_ARG(grid < (1LL << 31), "%s: grid too large", name);
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16)
+    rc = chlast ? launch_cfg<bf16_t, bf16_t, true>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s)
+                : launch_cfg<bf16_t, bf16_t, false>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s);
+  else if (dtype_in == IC2_F32 && dtype_out == IC2_F32)
+    rc = chlast ? launch_cfg<float, float, true>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s)
+                : launch_cfg<float, float, false>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s);
+  else {
+    set_error("%s: unsupported dtype pair %d -> %d", name, dtype_in, dtype_out);
+    return IC2_E_INVALID;
+  }
+  if (rc != IC2_OK) {
+    set_error("%s: no fused instance for up=%d down=%d taps=%d/%d", name, up, down, fu_taps, fd_taps);
+    return rc;
+  }
+  IC2_CHECK_LAUNCH(name);
+  return IC2_OK;
+}
+
+}  // namespace ic2
+
+using namespace ic2;
+
+extern "C" int ic2_filtered_lrelu(const void* x, void* y, int dtype, int64_t n, int64_t c, int in_h, int in_w,
+                                  int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps,
+                                  const float* b, int up, int down, int px0, int px1, int py0, int py1, float gain,
+                                  float slope, float clamp, int flip, void* stream) {
+  IC2_CHECK_ARG(n < (1 << 30) && c < (1 << 30), "filtered_lrelu: sizes too large");
+  return flrelu_common(x, y, dtype, dtype, false, (int)n, (int)c, (int)c, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
+                       fd_taps, b, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, nullptr, stream,
+                       "filtered_lrelu");
+}
+
+extern "C" int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_out, int n, int c_p, int in_h,
+                               int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd,
+                               int fd_taps, const float* b, int up, int down, int px0, int px1, int py0, int py1,
+                               float gain, float slope, float clamp, int flip, const float* post_scale,
+                               void* stream) {
+  IC2_CHECK_ARG(c_p % FLR_CPB == 0, "flrelu_nhwc: c_p must be a multiple of %d", FLR_CPB);
+  return flrelu_common(x, y, dtype_in, dtype_out, true, n, c_p, c_p, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
+                       fd_taps, b, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, post_scale, stream,
+                       "flrelu_nhwc");
+}

@@ -1,0 +1,390 @@
+// StyleGAN3 synthesis support kernels [SG3-public; call sites /root/reference/stylegan3_hvae_full.py:274,329]:
+//   bias_act (generic), upfirdn2d (generic NCHW), FullyConnectedLayer / nn.Linear, weight packing for the
+//   MFMA implicit GEMM, modulated_conv2d's (de)modulation coefficients, SynthesisInput Fourier features.
+#include "common.h"
+
+namespace ic2 {
+
+// ------------------------------------------------------------------------------------------------
+// bias_act: x viewed as [outer, c, inner]
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) bias_act_kernel(const T* __restrict__ x, const float* __restrict__ b,
+                                                       T* __restrict__ y, int64_t total, int64_t c, int64_t inner,
+                                                       int act, float alpha, float gain, float clamp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    float v = ld(x + i);
+    if (b) v += b[(i / inner) % c];
+    if (act == IC2_ACT_LRELU) v = v < 0.f ? v * alpha : v;
+    if (gain != 1.f) v *= gain;
+    if (clamp >= 0.f) v = fminf(fmaxf(v, -clamp), clamp);
+    st(y + i, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// upfirdn2d, direct form: out[oy][ox] = sum_{ty,tx} v[oy*dy+ty][ox*dx+tx] * g[ty][tx]
+//   v = pad(zero-insert(x)), g = flip(f) * gain (unless flip_filter); only taps that land on a
+//   non-inserted sample are visited (stride up).  One thread per output pixel.
+// ------------------------------------------------------------------------------------------------
+struct UfdArgs {
+  int64_t nc;
+  int in_h, in_w, out_h, out_w;
+  int f_ndim, f_h, f_w;
+  int upx, upy, downx, downy, px0, py0;
+  int flip;
+  float gain_x, gain_y;  // per-axis gains (separable) or gain_x = gain, gain_y = 1 (2-D)
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) upfirdn2d_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                        const float* __restrict__ f, UfdArgs a) {
+  const int64_t total = a.nc * a.out_h * a.out_w;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int fh = a.f_ndim == 1 ? a.f_w : a.f_h;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int ox = (int)(i % a.out_w);
+    const int oy = (int)((i / a.out_w) % a.out_h);
+    const int64_t pl = i / ((int64_t)a.out_w * a.out_h);
+    const T* xp = x + pl * a.in_h * a.in_w;
+    float acc = 0.f;
+    for (int ty = 0; ty < fh; ++ty) {
+      const int vy = oy * a.downy + ty - a.py0;  // position on the zero-inserted grid
+      if (vy < 0 || vy % a.upy) continue;
+      const int iy = vy / a.upy;
+      if (iy >= a.in_h) continue;
+      const int fy = a.flip ? ty : fh - 1 - ty;
+      for (int tx = 0; tx < a.f_w; ++tx) {
+        const int vx = ox * a.downx + tx - a.px0;
+        if (vx < 0 || vx % a.upx) continue;
+        const int ix = vx / a.upx;
+        if (ix >= a.in_w) continue;
+        const int fx = a.flip ? tx : a.f_w - 1 - tx;
+        float g;
+        if (f == nullptr) g = 1.f;
+        else if (a.f_ndim == 1) g = (f[fy] * a.gain_y) * (f[fx] * a.gain_x);
+        else g = f[fy * a.f_w + fx] * a.gain_x;
+        acc += ld(xp + (int64_t)iy * a.in_w + ix) * g;
+      }
+    }
+    st(y + i, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fully connected: one wave per output feature, lanes over the input features, 8 samples at a time
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                                 const float* __restrict__ b, float* __restrict__ y, int n, int in_f,
+                                                 int out_f, float w_gain, float b_gain, int act, float alpha,
+                                                 float act_gain) {
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= out_f) return;
+  const float* wr = w + (int64_t)o * in_f;
+  for (int n0 = 0; n0 < n; n0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int i = lane; i < in_f; i += 64) {
+      const float wv = wr[i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (n0 + k < n) acc[k] += x[(int64_t)(n0 + k) * ldx + i] * wv;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      acc[k] = v;
+    }
+    if (lane < 8 && n0 + lane < n) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k == lane) v = acc[k];
+      v = v * w_gain + (b ? b[o] * b_gain : 0.f);
+      if (act == IC2_ACT_LRELU) v = (v < 0.f ? v * alpha : v) * act_gain;
+      y[(int64_t)(n0 + lane) * out_f + o] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight packing [cout][cin][kh][kw] f32 -> [cout_p][kh][kw][cin_p] (dtype); optional pre-normalisation
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int kh,
+                                                          int kw, int cout_p, int cin_p, int prenorm, float gscale,
+                                                          T* __restrict__ out, float* __restrict__ wsq) {
+  const int o = blockIdx.x;
+  const int kk = kh * kw;
+  const int per = cin * kk;
+  __shared__ float red[256];
+  float scale = 1.f;
+  if (o < cout && prenorm) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < per; i += 256) {
+      const float v = w[(int64_t)o * per + i];
+      s += v * v;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    scale = rsqrtf(red[0] / (float)per);
+  }
+  const int total = kk * cin_p;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int i = e % cin_p;
+    const int k = e / cin_p;
+    float v = 0.f;
+    if (o < cout && i < cin) v = w[((int64_t)o * cin + i) * kk + k] * scale * gscale;
+    st(out + (int64_t)o * total + e, v);
+  }
+  if (wsq && o < cout) {
+    for (int i = threadIdx.x; i < cin; i += 256) {
+      float s = 0.f;
+      for (int k = 0; k < kk; ++k) {
+        const float v = w[((int64_t)o * cin + i) * kk + k] * scale;
+        s += v * v;
+      }
+      wsq[(int64_t)o * cin + i] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// modulation / demodulation coefficients
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) style_norm_kernel(const float* __restrict__ s, int64_t total,
+                                                         float* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < total; i += 256) acc += (double)s[i] * (double)s[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = rsqrtf((float)(red[0] / (double)total));
+}
+
+__global__ void __launch_bounds__(256) xscale_kernel(const float* __restrict__ s, int n, int cin, int cin_p,
+                                                     const float* __restrict__ snorm, float style_gain,
+                                                     float* __restrict__ xs) {
+  const int64_t total = (int64_t)n * cin_p;
+  const float g = snorm ? snorm[0] : style_gain;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int i = (int)(e % cin_p);
+    const int64_t nn = e / cin_p;
+    xs[e] = i < cin ? s[nn * cin + i] * g : 0.f;
+  }
+}
+
+// one wave per (n, o): lanes over cin
+__global__ void __launch_bounds__(256) oscale_kernel(const float* __restrict__ xs, const float* __restrict__ wsq,
+                                                     int n, int cin, int cin_p, int cout, int cout_p, int demod,
+                                                     float input_gain, float* __restrict__ os) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= (int64_t)n * cout_p) return;
+  const int o = (int)(item % cout_p);
+  const int64_t nn = item / cout_p;
+  if (o >= cout) {
+    if (lane == 0) os[item] = 0.f;
+    return;
+  }
+  if (!demod) {
+    if (lane == 0) os[item] = input_gain;
+    return;
+  }
+  float acc = 0.f;
+  for (int i = lane; i < cin; i += 64) {
+    const float v = xs[nn * cin_p + i];
+    acc += v * v * wsq[(int64_t)o * cin + i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) os[item] = input_gain * rsqrtf(acc + 1e-8f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// SynthesisInput Fourier features (NHWC)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) synth_input_kernel(const float* __restrict__ t, const float* __restrict__ freqs,
+                                                          const float* __restrict__ phases,
+                                                          const float* __restrict__ tr, int n, int c, int c_p,
+                                                          int size, float sr, float bw, T* __restrict__ out) {
+  const int64_t total = (int64_t)n * size * size * c_p;
+  const float theta = 0.5f * (float)size / sr;
+  const float two_pi = 6.283185307179586f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(e % c_p);
+    const int64_t pix = e / c_p;
+    const int xx = (int)(pix % size);
+    const int yy = (int)((pix / size) % size);
+    const int nn = (int)(pix / ((int64_t)size * size));
+    if (ch >= c) {
+      st(out + e, 0.f);
+      continue;
+    }
+    // t' = t / |t[:2]|
+    const float* tn = t + nn * 4;
+    const float nrm = sqrtf(tn[0] * tn[0] + tn[1] * tn[1]);
+    const float rc = tn[0] / nrm, rs = tn[1] / nrm, tx = tn[2] / nrm, ty = tn[3] / nrm;
+    // m_r @ m_t, then @ user transform tr (3x3)
+    const float A[3][3] = {{rc, -rs, -rc * tx + rs * ty}, {rs, rc, -rs * tx - rc * ty}, {0.f, 0.f, 1.f}};
+    float M[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) M[r][q] = A[r][0] * tr[0 * 3 + q] + A[r][1] * tr[1 * 3 + q] + A[r][2] * tr[2 * 3 + q];
+    const float f0 = freqs[ch * 2 + 0], f1 = freqs[ch * 2 + 1];
+    const float ph = phases[ch] + (f0 * M[0][2] + f1 * M[1][2]);
+    const float g0 = f0 * M[0][0] + f1 * M[1][0];
+    const float g1 = f0 * M[0][1] + f1 * M[1][1];
+    const float amp = fminf(fmaxf(1.f - (sqrtf(g0 * g0 + g1 * g1) - bw) / (sr * 0.5f - bw), 0.f), 1.f);
+    // affine_grid(align_corners=False): base coordinate (2j+1)/size - 1, scaled by theta
+    const float gx = ((2.f * xx + 1.f) / (float)size - 1.f) * theta;
+    const float gy = ((2.f * yy + 1.f) / (float)size - 1.f) * theta;
+    const float arg = (gx * g0 + gy * g1) + ph;
+    st(out + e, sinf(arg * two_pi) * amp);
+  }
+}
+
+static int grid_1d(int64_t total) {
+  int64_t g = ceil_div(total, 256);
+  if (g < 1) g = 1;
+  if (g > 4096) g = 4096;
+  return (int)g;
+}
+
+}  // namespace ic2
+
+using namespace ic2;
+
+extern "C" int ic2_bias_act(const void* x, const float* b, void* y, int dtype, int64_t outer, int64_t c, int64_t inner,
+                            int act, float alpha, float gain, float clamp, void* stream) {
+  IC2_CHECK_ARG(x && y && outer >= 0 && c >= 1 && inner >= 1, "bias_act: bad arguments");
+  IC2_CHECK_ARG(act == IC2_ACT_LINEAR || act == IC2_ACT_LRELU, "bias_act: unknown act %d", act);
+  const int64_t total = outer * c * inner;
+  if (total == 0) return IC2_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(bias_act_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, (const float*)x, b, (float*)y,
+                       total, c, inner, act, alpha, gain, clamp);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(bias_act_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, (const bf16_t*)x, b,
+                       (bf16_t*)y, total, c, inner, act, alpha, gain, clamp);
+  else
+    IC2_CHECK_ARG(false, "bias_act: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("bias_act");
+  return IC2_OK;
+}
+
+extern "C" int ic2_upfirdn2d(const void* x, void* y, int dtype, int64_t nc, int in_h, int in_w, int out_h, int out_w,
+                             const float* f, int f_ndim, int f_h, int f_w, int up_x, int up_y, int down_x, int down_y,
+                             int px0, int px1, int py0, int py1, int flip, float gain, void* stream) {
+  IC2_CHECK_ARG(x && y && nc >= 0 && in_h > 0 && in_w > 0, "upfirdn2d: bad arguments");
+  IC2_CHECK_ARG(up_x >= 1 && up_y >= 1 && down_x >= 1 && down_y >= 1, "upfirdn2d: bad scaling");
+  if (f == nullptr) {
+    f_ndim = 2;
+    f_h = f_w = 1;
+  }
+  IC2_CHECK_ARG((f_ndim == 1 && f_w >= 1) || (f_ndim == 2 && f_h >= 1 && f_w >= 1), "upfirdn2d: bad filter shape");
+  const int fh = f_ndim == 1 ? f_w : f_h;
+  const int ew = (in_w * up_x + px0 + px1 - f_w + down_x) / down_x;
+  const int eh = (in_h * up_y + py0 + py1 - fh + down_y) / down_y;
+  IC2_CHECK_ARG(out_w == ew && out_h == eh, "upfirdn2d: output %dx%d, expected %dx%d", out_h, out_w, eh, ew);
+  IC2_CHECK_ARG(out_w > 0 && out_h > 0, "upfirdn2d: empty output");
+  UfdArgs a;
+  a.nc = nc; a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w;
+  a.f_ndim = f_ndim; a.f_h = fh; a.f_w = f_w;
+  a.upx = up_x; a.upy = up_y; a.downx = down_x; a.downy = down_y; a.px0 = px0; a.py0 = py0; a.flip = flip;
+  if (f_ndim == 1) {
+    a.gain_x = sqrtf(gain);
+    a.gain_y = sqrtf(gain);
+  } else {
+    a.gain_x = gain;
+    a.gain_y = 1.f;
+  }
+  const int64_t total = nc * out_h * out_w;
+  if (total == 0) return IC2_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(upfirdn2d_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, (const float*)x, (float*)y, f, a);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(upfirdn2d_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+                       f, a);
+  else
+    IC2_CHECK_ARG(false, "upfirdn2d: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("upfirdn2d");
+  return IC2_OK;
+}
+
+extern "C" int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y, int n, int in_f,
+                      int out_f, float w_gain, float b_gain, int act, float alpha, float act_gain, void* stream) {
+  IC2_CHECK_ARG(x && w && y && n > 0 && in_f > 0 && out_f > 0 && ldx >= in_f, "fc: bad arguments");
+  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)ceil_div(out_f, 4)), dim3(256), 0, as_stream(stream), x, ldx, w, b, y, n,
+                     in_f, out_f, w_gain, b_gain, act, alpha, act_gain);
+  IC2_CHECK_LAUNCH("fc");
+  return IC2_OK;
+}
+
+extern "C" int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
+                               float scale, void* w_out, int dtype, float* wsq_out, void* stream) {
+  IC2_CHECK_ARG(w && w_out && cout > 0 && cin > 0 && kh > 0 && kw > 0 && cout_p >= cout && cin_p >= cin,
+                "pack_weight: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p, cin_p,
+                       prenorm, scale, (float*)w_out, wsq_out);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p, cin_p,
+                       prenorm, scale, (bf16_t*)w_out, wsq_out);
+  else
+    IC2_CHECK_ARG(false, "pack_weight: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("pack_weight");
+  return IC2_OK;
+}
+
+extern "C" int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int cout, int cin_p, int cout_p,
+                                int demod, float style_gain, float input_gain, float* xscale_out, float* oscale_out,
+                                float* scratch, void* stream) {
+  IC2_CHECK_ARG(styles && xscale_out && oscale_out && n > 0 && cin > 0 && cout > 0, "modconv_prep: bad arguments");
+  IC2_CHECK_ARG(!demod || (wsq && scratch), "modconv_prep: demodulation needs wsq and scratch");
+  hipStream_t s = as_stream(stream);
+  if (demod) hipLaunchKernelGGL(style_norm_kernel, dim3(1), dim3(256), 0, s, styles, (int64_t)n * cin, scratch);
+  hipLaunchKernelGGL(xscale_kernel, dim3(grid_1d((int64_t)n * cin_p)), dim3(256), 0, s, styles, n, cin, cin_p,
+                     demod ? scratch : nullptr, style_gain, xscale_out);
+  hipLaunchKernelGGL(oscale_kernel, dim3((unsigned)ceil_div((int64_t)n * cout_p, 4)), dim3(256), 0, s, xscale_out, wsq,
+                     n, cin, cin_p, cout, cout_p, demod, input_gain, oscale_out);
+  IC2_CHECK_LAUNCH("modconv_prep");
+  return IC2_OK;
+}
+
+extern "C" int ic2_synth_input_features(const float* t, const float* freqs, const float* phases, const float* transform,
+                                        int n, int c, int c_p, int size, float sampling_rate, float bandwidth,
+                                        void* x_out, int dtype, void* stream) {
+  IC2_CHECK_ARG(t && freqs && phases && transform && x_out && n > 0 && c > 0 && c_p >= c && size > 0,
+                "synth_input_features: bad arguments");
+  const int64_t total = (int64_t)n * size * size * c_p;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(synth_input_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, t, freqs, phases, transform,
+                       n, c, c_p, size, sampling_rate, bandwidth, (float*)x_out);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(synth_input_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, t, freqs, phases, transform,
+                       n, c, c_p, size, sampling_rate, bandwidth, (bf16_t*)x_out);
+  else
+    IC2_CHECK_ARG(false, "synth_input_features: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("synth_input_features");
+  return IC2_OK;
+}

@@ -1,0 +1,68 @@
+"""Batch-sharded data parallelism: one process per GPU, contiguous batch slices,
+no data-path collective; one all_reduce(SUM) of a small fp64 metric vector per batch over RCCL
+(backend "nccl" on ROCm) -- gloo on CPU for tests.  The reference has no distributed code."""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init(backend=None):
+    """Initialise the default process group from torchrun's env (no-op for world size 1)."""
+    rank, world, local = env_rank_world()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+def shard(n_total, rank, world):
+    """Contiguous slice [start, stop) of a global batch for `rank` (sizes differ by at most 1)."""
+    base, rem = divmod(n_total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def metric_vector(sse_sum, n_values, n_images, hist=None, extra=()):
+    """[sum SSE_uint8, n_pixels, n_images, *extra, *hist] as float64 (the all-reduced record)."""
+    parts = [torch.tensor([float(sse_sum), float(n_values), float(n_images), *map(float, extra)], dtype=torch.float64)]
+    if hist is not None:
+        parts.append(hist.detach().to("cpu", torch.float64).reshape(-1))
+    return torch.cat(parts)
+
+
+def allreduce_sum(vec, device=None):
+    """all_reduce(SUM) of a small fp64 vector (identity when not distributed)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return vec
+    t = vec.to(device) if device is not None else vec
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.to(vec.device)
+
+
+def allreduce_max(value, device=None):
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(device=None):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if device is not None and device.type == "cuda":
+            dist.barrier(device_ids=[device.index])
+        else:
+            dist.barrier()

@@ -1,0 +1,479 @@
+"""MI355X-native StyleGAN3-T generator: the ``G_ema`` duck type the reference decodes with.
+
+The reference unpickles NVlabs' ``G_ema`` (/root/reference/stylegan3_hvae_full.py:454-455) and calls
+``G.synthesis(ws, noise_mode=...)`` (``:274, :329``; ``gumbel_softmax_compression.py:193, 262``),
+``G.mapping`` / ``G.mapping.w_avg`` (``:557, :626``), ``G(z, c)`` (``:561``), ``G.parameters()``
+(``:262``) and ``.z_dim/.w_dim/.num_ws/.img_resolution/.img_channels`` (``:459-468``).  This module
+provides the same module tree (state-dict keys ``synthesis.L0_36_512.affine.weight`` ...), the same
+seeded parameter construction order, and a forward that runs entirely in libic2ops HIP kernels:
+
+    per layer:  styles = FC(w)                        ic2_fc
+                xscale / oscale (mod / demod)         ic2_modconv_prep
+                y = oscale * conv(W_norm, x) + bias   ic2_conv_igemm   (MFMA, NHWC)
+                x = filtered_lrelu(y) * xscale_next   ic2_flrelu_nhwc  (fused FIR, NHWC)
+
+``precision='bf16'`` stores activations and weights in bf16 (fp32 accumulate, fp32 FIR math);
+``precision='fp32'`` (default) is the parity mode (exact-fp32 MFMA).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import scipy.signal
+import torch
+
+from . import _native as nv
+from . import sg3_ops
+
+
+def _version_key(*tensors):
+    return tuple((t.data_ptr(), t._version, t.device) for t in tensors)
+
+
+# ------------------------------------------------------------------------------------------------
+class FullyConnectedLayer(torch.nn.Module):
+    """[SG3-public] y = x @ (W * lr/sqrt(in))^T + b * lr, optional lrelu (bias_act)."""
+
+    def __init__(self, in_features, out_features, activation="linear", bias=True, lr_multiplier=1, weight_init=1,
+                 bias_init=0):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.activation = activation
+        self.weight = torch.nn.Parameter(torch.randn([out_features, in_features]) * (weight_init / lr_multiplier))
+        bias_init = np.broadcast_to(np.asarray(bias_init, dtype=np.float32), [out_features])
+        self.bias = torch.nn.Parameter(torch.from_numpy(bias_init / lr_multiplier)) if bias else None
+        self.weight_gain = lr_multiplier / np.sqrt(in_features)
+        self.bias_gain = lr_multiplier
+
+    def run(self, x, out=None, ldx=None, n=None):
+        """x: f32 [n, ldx] rows (only the first in_features of each row are read)."""
+        n = x.shape[0] if n is None else n
+        ldx = self.in_features if ldx is None else ldx
+        if out is None:
+            out = torch.empty([n, self.out_features], dtype=torch.float32, device=x.device)
+        act = nv.ACT_LRELU if self.activation == "lrelu" else nv.ACT_LINEAR
+        nv.call("ic2_fc", nv.ptr(x), ldx, nv.ptr(self.weight), nv.ptr(self.bias), nv.ptr(out), n, self.in_features,
+                self.out_features, float(self.weight_gain), float(self.bias_gain), act, 0.2,
+                float(np.sqrt(2)) if act == nv.ACT_LRELU else 1.0, nv.stream_of(x))
+        return out
+
+    def forward(self, x):
+        x = x.to(torch.float32).contiguous()
+        nv.require_gpu(x)
+        if self.activation not in ("linear", "lrelu"):
+            raise NotImplementedError(self.activation)
+        return self.run(x)
+
+    def extra_repr(self):
+        return f"in_features={self.in_features:d}, out_features={self.out_features:d}, activation={self.activation:s}"
+
+
+# ------------------------------------------------------------------------------------------------
+class MappingNetwork(torch.nn.Module):
+    """[SG3-public] z -> w (2 lrelu FCs, lr 0.01), w_avg, truncation.  Not on the encode->decode path
+    (SURVEY.md 2 #9); provided for the Generator duck type (``G.mapping``, ``G.mapping.w_avg``)."""
+
+    def __init__(self, z_dim, c_dim, w_dim, num_ws, num_layers=2, lr_multiplier=0.01, w_avg_beta=0.998):
+        super().__init__()
+        if c_dim:
+            raise NotImplementedError("conditional mapping (c_dim > 0) is not on the path")
+        self.z_dim, self.c_dim, self.w_dim, self.num_ws = z_dim, c_dim, w_dim, num_ws
+        self.num_layers, self.w_avg_beta = num_layers, w_avg_beta
+        features = [z_dim] + [w_dim] * num_layers
+        for idx, in_f, out_f in zip(range(num_layers), features[:-1], features[1:]):
+            setattr(self, f"fc{idx}", FullyConnectedLayer(in_f, out_f, activation="lrelu", lr_multiplier=lr_multiplier))
+        self.register_buffer("w_avg", torch.zeros([w_dim]))
+
+    def forward(self, z, c=None, truncation_psi=1, truncation_cutoff=None, update_emas=False):
+        if update_emas:
+            raise NotImplementedError("update_emas is a training feature (out of scope)")
+        x = z.to(torch.float32).contiguous()
+        nv.require_gpu(x)
+        x = x * (x.square().mean(1, keepdim=True) + 1e-8).rsqrt()
+        for idx in range(self.num_layers):
+            x = getattr(self, f"fc{idx}").run(x.contiguous())
+        x = x.unsqueeze(1).repeat([1, self.num_ws, 1])
+        if truncation_psi != 1:
+            cut = self.num_ws if truncation_cutoff is None else truncation_cutoff
+            x[:, :cut] = self.w_avg.lerp(x[:, :cut], truncation_psi)
+        return x
+
+
+# ------------------------------------------------------------------------------------------------
+class SynthesisInput(torch.nn.Module):
+    """[SG3-public] Fourier-feature input; buffers/params drawn in SG3's order."""
+
+    def __init__(self, w_dim, channels, size, sampling_rate, bandwidth):
+        super().__init__()
+        self.w_dim = w_dim
+        self.channels = channels
+        self.size = np.broadcast_to(np.asarray(size), [2])
+        self.sampling_rate = sampling_rate
+        self.bandwidth = bandwidth
+        freqs = torch.randn([self.channels, 2])
+        radii = freqs.square().sum(dim=1, keepdim=True).sqrt()
+        freqs /= radii * radii.square().exp().pow(0.25)
+        freqs *= bandwidth
+        phases = torch.rand([self.channels]) - 0.5
+        self.weight = torch.nn.Parameter(torch.randn([self.channels, self.channels]))
+        self.affine = FullyConnectedLayer(w_dim, 4, weight_init=0, bias_init=[1, 0, 0, 0])
+        self.register_buffer("transform", torch.eye(3, 3))
+        self.register_buffer("freqs", freqs)
+        self.register_buffer("phases", phases)
+        self._cache = {}
+
+    def packed_weight(self, dt):
+        key = (dt, _version_key(self.weight))
+        hit = self._cache.get(dt)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        C, cp = self.channels, nv.pad32(self.channels)
+        w = self.weight.detach().to(torch.float32).contiguous()
+        out = torch.empty([cp, cp], dtype=dt, device=w.device)
+        nv.call("ic2_pack_weight", nv.ptr(w), C, C, 1, 1, cp, cp, 0, float(1 / np.sqrt(C)), nv.ptr(out),
+                nv.dtype_code(dt), None, nv.stream_of(w))
+        self._cache[dt] = (key, out)
+        return out
+
+    def run_nhwc(self, ws, ldx, n, dt, post_scale):
+        """Features -> NHWC [n, S, S, c_p] (dt), scaled by the first layer's xscale (post_scale)."""
+        C, cp, S = self.channels, nv.pad32(self.channels), int(self.size[0])
+        dev = ws.device
+        t = self.affine.run(ws, ldx=ldx, n=n)
+        feats = torch.empty([n, S, S, cp], dtype=dt, device=dev)
+        nv.call("ic2_synth_input_features", nv.ptr(t), nv.ptr(self.freqs), nv.ptr(self.phases), nv.ptr(self.transform),
+                n, C, cp, S, float(self.sampling_rate), float(self.bandwidth), nv.ptr(feats), nv.dtype_code(dt),
+                nv.stream_of(ws))
+        out = torch.empty([n, S, S, cp], dtype=dt, device=dev)
+        w = self.packed_weight(dt)
+        nv.call("ic2_conv_igemm", nv.ptr(feats), nv.ptr(w), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, S, S,
+                cp, cp, C, 1, 1, 0, S, S, nv.ptr(post_scale), None, 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(ws))
+        return out
+
+    def forward(self, w):
+        w = w.to(torch.float32).contiguous()
+        nv.require_gpu(w)
+        n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad32(self.channels)
+        x = self.run_nhwc(w, self.w_dim, n, torch.float32, None)
+        y = torch.empty([n, C, S, S], dtype=torch.float32, device=w.device)
+        nv.call("ic2_nhwc_to_nchw", nv.ptr(x), nv.F32, nv.ptr(y), n, C, S, S, cp, nv.stream_of(w))
+        return y
+
+    def extra_repr(self):
+        return (f"w_dim={self.w_dim:d}, channels={self.channels:d}, size={list(self.size)}, "
+                f"sampling_rate={self.sampling_rate:g}, bandwidth={self.bandwidth:g}")
+
+
+# ------------------------------------------------------------------------------------------------
+class SynthesisLayer(torch.nn.Module):
+    """[SG3-public] modulated conv + filtered lrelu; same constructor and derived hyper-parameters."""
+
+    def __init__(self, w_dim, is_torgb, is_critically_sampled, use_fp16, in_channels, out_channels, in_size, out_size,
+                 in_sampling_rate, out_sampling_rate, in_cutoff, out_cutoff, in_half_width, out_half_width,
+                 conv_kernel=3, filter_size=6, lrelu_upsampling=2, use_radial_filters=False, conv_clamp=256,
+                 magnitude_ema_beta=0.999):
+        super().__init__()
+        if use_radial_filters and not is_critically_sampled and not is_torgb:
+            raise NotImplementedError("radial (StyleGAN3-R) filters are not on the path: StyleGAN3-T only")
+        self.w_dim = w_dim
+        self.is_torgb = is_torgb
+        self.is_critically_sampled = is_critically_sampled
+        self.use_fp16 = use_fp16
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.in_size = np.broadcast_to(np.asarray(in_size), [2])
+        self.out_size = np.broadcast_to(np.asarray(out_size), [2])
+        self.in_sampling_rate = in_sampling_rate
+        self.out_sampling_rate = out_sampling_rate
+        self.tmp_sampling_rate = max(in_sampling_rate, out_sampling_rate) * (1 if is_torgb else lrelu_upsampling)
+        self.in_cutoff = in_cutoff
+        self.out_cutoff = out_cutoff
+        self.in_half_width = in_half_width
+        self.out_half_width = out_half_width
+        self.conv_kernel = 1 if is_torgb else conv_kernel
+        self.conv_clamp = conv_clamp
+        self.magnitude_ema_beta = magnitude_ema_beta
+
+        self.affine = FullyConnectedLayer(self.w_dim, self.in_channels, bias_init=1)
+        self.weight = torch.nn.Parameter(torch.randn([self.out_channels, self.in_channels, self.conv_kernel,
+                                                      self.conv_kernel]))
+        self.bias = torch.nn.Parameter(torch.zeros([self.out_channels]))
+        self.register_buffer("magnitude_ema", torch.ones([]))
+
+        self.up_factor = int(np.rint(self.tmp_sampling_rate / self.in_sampling_rate))
+        assert self.in_sampling_rate * self.up_factor == self.tmp_sampling_rate
+        self.up_taps = filter_size * self.up_factor if self.up_factor > 1 and not self.is_torgb else 1
+        self.register_buffer("up_filter", self.design_lowpass_filter(
+            numtaps=self.up_taps, cutoff=self.in_cutoff, width=self.in_half_width * 2, fs=self.tmp_sampling_rate))
+        self.down_factor = int(np.rint(self.tmp_sampling_rate / self.out_sampling_rate))
+        assert self.out_sampling_rate * self.down_factor == self.tmp_sampling_rate
+        self.down_taps = filter_size * self.down_factor if self.down_factor > 1 and not self.is_torgb else 1
+        self.down_radial = use_radial_filters and not self.is_critically_sampled
+        self.register_buffer("down_filter", self.design_lowpass_filter(
+            numtaps=self.down_taps, cutoff=self.out_cutoff, width=self.out_half_width * 2, fs=self.tmp_sampling_rate))
+
+        pad_total = (self.out_size - 1) * self.down_factor + 1
+        pad_total -= (self.in_size + self.conv_kernel - 1) * self.up_factor
+        pad_total += self.up_taps + self.down_taps - 2
+        pad_lo = (pad_total + self.up_factor) // 2
+        pad_hi = pad_total - pad_lo
+        self.padding = [int(pad_lo[0]), int(pad_hi[0]), int(pad_lo[1]), int(pad_hi[1])]
+
+        # host copies of the (constant) FIR taps: the fused kernel takes them by value
+        self._fu = None if self.up_filter is None else np.ascontiguousarray(self.up_filter.numpy(), np.float32)
+        self._fd = None if self.down_filter is None else np.ascontiguousarray(self.down_filter.numpy(), np.float32)
+        self._cache = {}
+        self._ig_cache = None
+
+    # ---- constants -------------------------------------------------------------------------
+    @property
+    def cin_p(self):
+        return nv.pad32(self.in_channels)
+
+    @property
+    def cout_p(self):
+        return nv.pad32(self.out_channels)
+
+    def input_gain(self):
+        key = _version_key(self.magnitude_ema)
+        if self._ig_cache is None or self._ig_cache[0] != key:
+            self._ig_cache = (key, float(self.magnitude_ema.detach().float().rsqrt().cpu()))
+        return self._ig_cache[1]
+
+    def packed(self, dt):
+        """(W packed [cout_p][k][k][cin_p] dt, wsq [cout][cin] f32, bias_p [cout_p] f32) per weight version."""
+        key = (dt, _version_key(self.weight, self.bias))
+        hit = self._cache.get(dt)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w = self.weight.detach().to(torch.float32).contiguous()
+        k = self.conv_kernel
+        wp = torch.empty([self.cout_p, k, k, self.cin_p], dtype=dt, device=w.device)
+        wsq = torch.empty([self.out_channels, self.in_channels], dtype=torch.float32, device=w.device)
+        nv.call("ic2_pack_weight", nv.ptr(w), self.out_channels, self.in_channels, k, k, self.cout_p, self.cin_p,
+                int(not self.is_torgb), 1.0, nv.ptr(wp), nv.dtype_code(dt), nv.ptr(wsq), nv.stream_of(w))
+        bp = torch.zeros([self.cout_p], dtype=torch.float32, device=w.device)
+        bp[: self.out_channels] = self.bias.detach().float()
+        val = (wp, wsq, bp)
+        self._cache[dt] = (key, val)
+        return val
+
+    def scales(self, ws, ldx, n, dt):
+        """Runs the affine FC and the (de)modulation prep: -> (xscale [n][cin_p], oscale [n][cout_p])."""
+        dev = ws.device
+        styles = self.affine.run(ws, ldx=ldx, n=n)
+        _, wsq, _ = self.packed(dt)
+        xs = torch.empty([n, self.cin_p], dtype=torch.float32, device=dev)
+        os_ = torch.empty([n, self.cout_p], dtype=torch.float32, device=dev)
+        scratch = torch.empty([4], dtype=torch.float32, device=dev)
+        style_gain = float(1 / np.sqrt(self.in_channels * (self.conv_kernel ** 2))) if self.is_torgb else 1.0
+        nv.call("ic2_modconv_prep", nv.ptr(styles), nv.ptr(wsq), n, self.in_channels, self.out_channels, self.cin_p,
+                self.cout_p, int(not self.is_torgb), style_gain, self.input_gain(), nv.ptr(xs), nv.ptr(os_),
+                nv.ptr(scratch), nv.stream_of(ws))
+        return xs, os_
+
+    # ---- NHWC pipeline step ------------------------------------------------------------------
+    def run_nhwc(self, x, n, dt, oscale, post_scale, final_scale=None):
+        """x: NHWC [n, in, in, cin_p] already scaled by this layer's xscale.  Returns NHWC output scaled by
+        post_scale (next layer's xscale), or -- for ToRGB -- the final NCHW f32 image * final_scale."""
+        s_in = int(self.in_size[0])
+        k = self.conv_kernel
+        pad = k - 1
+        conv = s_in + 2 * pad - k + 1
+        wp, _, bp = self.packed(dt)
+        stream = nv.stream_of(x)
+        if self.is_torgb:
+            assert self.up_factor == 1 and self.down_factor == 1 and self.padding == [0, 0, 0, 0]
+            out = torch.empty([n, self.out_channels, conv, conv], dtype=torch.float32, device=x.device)
+            clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
+            nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(out), nv.dtype_code(dt), nv.F32, n, s_in, s_in,
+                    self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp),
+                    nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW, stream)
+            return out
+        y = torch.empty([n, conv, conv, self.cout_p], dtype=dt, device=x.device)
+        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(dt), n, s_in, s_in,
+                self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0, 0.0,
+                1.0, -1.0, 1.0, nv.NHWC, stream)
+        s_out = int(self.out_size[0])
+        out = torch.empty([n, s_out, s_out, self.cout_p], dtype=dt, device=x.device)
+        fu = self._fu
+        fd = self._fd
+        px0, px1, py0, py1 = self.padding
+        clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
+        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, self.cout_p, conv,
+                conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
+                1 if fu is None else fu.shape[0], None if fd is None else fd.ctypes.data_as(ctypes.c_void_p),
+                1 if fd is None else fd.shape[0], None, self.up_factor, self.down_factor, px0, px1, py0, py1,
+                float(np.sqrt(2)), 0.2, clamp, 0, nv.ptr(post_scale), stream)
+        return out
+
+    def forward(self, x, w, noise_mode="random", force_fp32=False, update_emas=False):
+        """Layer-level API (NCHW f32 in/out), as SG3's SynthesisLayer.forward."""
+        assert noise_mode in ("random", "const", "none")
+        if update_emas:
+            raise NotImplementedError("update_emas is a training feature (out of scope)")
+        x = x.to(torch.float32).contiguous()
+        w = w.to(torch.float32).contiguous()
+        nv.require_gpu(x, w)
+        n = x.shape[0]
+        assert list(x.shape) == [n, self.in_channels, int(self.in_size[1]), int(self.in_size[0])], x.shape
+        dt = torch.float32
+        xs, os_ = self.scales(w, self.w_dim, n, dt)
+        s_in = int(self.in_size[0])
+        xn = torch.empty([n, s_in, s_in, self.cin_p], dtype=dt, device=x.device)
+        nv.call("ic2_nchw_to_nhwc", nv.ptr(x), nv.ptr(xn), nv.F32, n, self.in_channels, s_in, s_in, self.cin_p,
+                nv.ptr(xs), nv.stream_of(x))
+        out = self.run_nhwc(xn, n, dt, os_, None)
+        if self.is_torgb:
+            return out
+        s_out = int(self.out_size[0])
+        y = torch.empty([n, self.out_channels, s_out, s_out], dtype=torch.float32, device=x.device)
+        nv.call("ic2_nhwc_to_nchw", nv.ptr(out), nv.F32, nv.ptr(y), n, self.out_channels, s_out, s_out, self.cout_p,
+                nv.stream_of(x))
+        return y
+
+    @staticmethod
+    def design_lowpass_filter(numtaps, cutoff, width, fs, radial=False):
+        assert numtaps >= 1
+        if numtaps == 1:
+            return None
+        if radial:
+            raise NotImplementedError("radial filters (StyleGAN3-R) are not on the path")
+        f = scipy.signal.firwin(numtaps=numtaps, cutoff=cutoff, width=width, fs=fs)
+        return torch.as_tensor(f, dtype=torch.float32)
+
+    def extra_repr(self):
+        return "\n".join([
+            f"w_dim={self.w_dim:d}, is_torgb={self.is_torgb},",
+            f"is_critically_sampled={self.is_critically_sampled}, use_fp16={self.use_fp16},",
+            f"in_sampling_rate={self.in_sampling_rate:g}, out_sampling_rate={self.out_sampling_rate:g},",
+            f"in_cutoff={self.in_cutoff:g}, out_cutoff={self.out_cutoff:g},",
+            f"in_half_width={self.in_half_width:g}, out_half_width={self.out_half_width:g},",
+            f"in_size={list(self.in_size)}, out_size={list(self.out_size)},",
+            f"in_channels={self.in_channels:d}, out_channels={self.out_channels:d}"])
+
+
+# ------------------------------------------------------------------------------------------------
+class SynthesisNetwork(torch.nn.Module):
+    """[SG3-public] ws [N, num_ws, w_dim] -> image [N, 3, R, R] f32, entirely in HIP kernels."""
+
+    def __init__(self, w_dim, img_resolution, img_channels, channel_base=32768, channel_max=512, num_layers=14,
+                 num_critical=2, first_cutoff=2, first_stopband=2 ** 2.1, last_stopband_rel=2 ** 0.3, margin_size=10,
+                 output_scale=0.25, num_fp16_res=4, precision="fp32", **layer_kwargs):
+        super().__init__()
+        self.w_dim = w_dim
+        self.num_ws = num_layers + 2
+        self.img_resolution = img_resolution
+        self.img_channels = img_channels
+        self.num_layers = num_layers
+        self.num_critical = num_critical
+        self.margin_size = margin_size
+        self.output_scale = output_scale
+        self.num_fp16_res = num_fp16_res
+        self.precision = precision
+        nv.torch_dtype(precision)
+
+        last_cutoff = self.img_resolution / 2
+        last_stopband = last_cutoff * last_stopband_rel
+        exponents = np.minimum(np.arange(self.num_layers + 1) / (self.num_layers - self.num_critical), 1)
+        cutoffs = first_cutoff * (last_cutoff / first_cutoff) ** exponents
+        stopbands = first_stopband * (last_stopband / first_stopband) ** exponents
+        sampling_rates = np.exp2(np.ceil(np.log2(np.minimum(stopbands * 2, self.img_resolution))))
+        half_widths = np.maximum(stopbands, sampling_rates / 2) - cutoffs
+        sizes = sampling_rates + self.margin_size * 2
+        sizes[-2:] = self.img_resolution
+        channels = np.rint(np.minimum((channel_base / 2) / cutoffs, channel_max))
+        channels[-1] = self.img_channels
+
+        self.input = SynthesisInput(w_dim=self.w_dim, channels=int(channels[0]), size=int(sizes[0]),
+                                    sampling_rate=sampling_rates[0], bandwidth=cutoffs[0])
+        self.layer_names = []
+        for idx in range(self.num_layers + 1):
+            prev = max(idx - 1, 0)
+            is_torgb = idx == self.num_layers
+            is_critically_sampled = idx >= self.num_layers - self.num_critical
+            use_fp16 = sampling_rates[idx] * (2 ** self.num_fp16_res) > self.img_resolution
+            layer = SynthesisLayer(
+                w_dim=self.w_dim, is_torgb=is_torgb, is_critically_sampled=is_critically_sampled, use_fp16=use_fp16,
+                in_channels=int(channels[prev]), out_channels=int(channels[idx]), in_size=int(sizes[prev]),
+                out_size=int(sizes[idx]), in_sampling_rate=int(sampling_rates[prev]),
+                out_sampling_rate=int(sampling_rates[idx]), in_cutoff=cutoffs[prev], out_cutoff=cutoffs[idx],
+                in_half_width=half_widths[prev], out_half_width=half_widths[idx], **layer_kwargs)
+            name = f"L{idx}_{layer.out_size[0]}_{layer.out_channels}"
+            setattr(self, name, layer)
+            self.layer_names.append(name)
+
+    def layers(self):
+        return [getattr(self, name) for name in self.layer_names]
+
+    def forward(self, ws, noise_mode="const", force_fp32=False, update_emas=False, **layer_kwargs):
+        """noise_mode is accepted and ignored exactly like SG3 (the T generator has no noise inputs)."""
+        assert noise_mode in ("random", "const", "none")
+        if update_emas:
+            raise NotImplementedError("update_emas is a training feature (out of scope)")
+        assert ws.ndim == 3 and ws.shape[1] == self.num_ws and ws.shape[2] == self.w_dim, ws.shape
+        ws = ws.to(torch.float32).contiguous()
+        nv.require_gpu(ws)
+        dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
+        n = ws.shape[0]
+        ldx = self.num_ws * self.w_dim
+        layers = self.layers()
+        # all per-layer modulation coefficients first (each step needs the next layer's xscale)
+        flat = ws.view(-1)
+        sc = [L.scales(flat[(i + 1) * self.w_dim:], ldx, n, dt) for i, L in enumerate(layers)]
+        x = self.input.run_nhwc(ws, ldx, n, dt, sc[0][0])
+        for i, L in enumerate(layers):
+            post = sc[i + 1][0] if i + 1 < len(layers) else None
+            x = L.run_nhwc(x, n, dt, sc[i][1], post, final_scale=self.output_scale if L.is_torgb else None)
+        return x
+
+    def extra_repr(self):
+        return "\n".join([
+            f"w_dim={self.w_dim:d}, num_ws={self.num_ws:d},",
+            f"img_resolution={self.img_resolution:d}, img_channels={self.img_channels:d},",
+            f"num_layers={self.num_layers:d}, num_critical={self.num_critical:d},",
+            f"margin_size={self.margin_size:d}, num_fp16_res={self.num_fp16_res:d}, precision={self.precision}"])
+
+
+# ------------------------------------------------------------------------------------------------
+class Generator(torch.nn.Module):
+    """[SG3-public] Generator(z_dim, c_dim, w_dim, img_resolution, img_channels): synthesis built first,
+    then mapping (SG3's construction order, so a seeded build draws the same parameters)."""
+
+    def __init__(self, z_dim=512, c_dim=0, w_dim=512, img_resolution=256, img_channels=3, mapping_kwargs={},
+                 precision="fp32", **synthesis_kwargs):
+        super().__init__()
+        self.z_dim = z_dim
+        self.c_dim = c_dim
+        self.w_dim = w_dim
+        self.img_resolution = img_resolution
+        self.img_channels = img_channels
+        self.synthesis = SynthesisNetwork(w_dim=w_dim, img_resolution=img_resolution, img_channels=img_channels,
+                                          precision=precision, **synthesis_kwargs)
+        self.num_ws = self.synthesis.num_ws
+        self.mapping = MappingNetwork(z_dim=z_dim, c_dim=c_dim, w_dim=w_dim, num_ws=self.num_ws, **mapping_kwargs)
+
+    @property
+    def precision(self):
+        return self.synthesis.precision
+
+    def set_precision(self, precision):
+        nv.torch_dtype(precision)
+        self.synthesis.precision = precision
+        return self
+
+    def forward(self, z, c=None, truncation_psi=1, truncation_cutoff=None, update_emas=False, **synthesis_kwargs):
+        ws = self.mapping(z, c, truncation_psi=truncation_psi, truncation_cutoff=truncation_cutoff,
+                          update_emas=update_emas)
+        return self.synthesis(ws, update_emas=update_emas, **synthesis_kwargs)
+
+
+def make_generator(img_resolution=256, seed=None, precision="fp32", device="cuda", **kw):
+    """Seeded StyleGAN3-T generator (random init -- no pretrained weights are available offline)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    G = Generator(z_dim=512, c_dim=0, w_dim=512, img_resolution=img_resolution, img_channels=3, precision=precision, **kw)
+    return G.to(device).eval().requires_grad_(False)

@@ -1,0 +1,334 @@
+"""Drop-in for /root/reference/stylegan3_hvae_full.py's hot-path classes, MI355X-native.
+
+Same class names, constructor arguments, module tree / state-dict keys and parameter-construction
+order as the reference (so ``torch.manual_seed(s)`` + construction draws identical weights and the
+reference's checkpoints load).  The forward passes run in libic2ops HIP kernels:
+
+  HVAE_VGG_Encoder.forward  (ref :105-167)   NHWC, MFMA implicit-GEMM 3x3 convs, deterministic GroupNorm,
+                                             fused GN-apply + lrelu + 2x2 avg-pool, GAP, FCs, reparam
+  StyleGAN3Compressor.compress (ref :295-318) bit-exact uniform quantizer kernel
+  StyleGAN3Compressor.decompress / forward    generator.synthesis (networks_stylegan3) + bilinear resize
+
+Behaviour kept on purpose: the fine projector's fc1 is re-created with fresh
+``nn.Linear`` weights (CPU RNG) whenever the pooled width differs from ``in_channels`` (ref :225-230);
+reparameterisation noise is drawn with ``torch.randn_like`` on the device in the reference's order.
+Not kept: the debug prints of every forward.  ``precision`` ('fp32' parity | 'bf16' throughput) is an
+opt-in extension.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from PIL import Image
+
+from . import _native as nv
+
+
+def _version_key(*tensors):
+    return tuple((t.data_ptr(), t._version, t.device) for t in tensors)
+
+
+class _Act:
+    """NHWC activation handle: tensor [n, h, w, c_p] + logical channel count."""
+    __slots__ = ("t", "n", "h", "w", "c", "c_p")
+
+    def __init__(self, t, c):
+        self.t = t
+        self.n, self.h, self.w, self.c_p = t.shape
+        self.c = c
+
+
+def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
+    """nn.Conv2d (3x3 or k x k, stride 1, 'same' padding) + bias on MFMA."""
+    cout, cin, kh, kw = conv.weight.shape
+    assert conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and cin == x.c
+    pad = conv.padding[0]
+    key = (dt, _version_key(conv.weight, conv.bias))
+    hit = cache.get(id(conv))
+    if hit is None or hit[0] != key:
+        w = conv.weight.detach().to(torch.float32).contiguous()
+        cout_p, cin_p = nv.pad32(cout), x.c_p
+        wp = torch.empty([cout_p, kh, kw, cin_p], dtype=dt, device=w.device)
+        nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(wp), nv.dtype_code(dt),
+                None, stream)
+        bp = torch.zeros([cout_p], dtype=torch.float32, device=w.device)
+        if conv.bias is not None:
+            bp[:cout] = conv.bias.detach().float()
+        hit = (key, (wp, bp))
+        cache[id(conv)] = hit
+    wp, bp = hit[1]
+    cout_p = wp.shape[0]
+    ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
+    y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
+    nv.call("ic2_conv_igemm", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.t.dtype), nv.dtype_code(dt), x.n, x.h,
+            x.w, x.c_p, cout_p, cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream)
+    return _Act(y, cout)
+
+
+def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2):
+    """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2))."""
+    groups = norm.num_groups
+    nfl = int(nv.query("ic2_group_norm_stats_floats", y.n, y.h * y.w, groups))
+    stats = torch.empty([nfl], dtype=torch.float32, device=y.t.device)
+    nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
+            float(norm.eps), nv.ptr(stats), stream)
+    oh, ow = (y.h // 2, y.w // 2) if pool else (y.h, y.w)
+    out = torch.empty([y.n, oh, ow, y.c_p], dtype=dt, device=y.t.device)
+    nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype), nv.dtype_code(dt), y.n, y.h, y.w,
+            y.c_p, y.c, groups, nv.ptr(stats), nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)
+    return _Act(out, y.c)
+
+
+def _gap(x: _Act, stream):
+    nfl = int(nv.query("ic2_global_avg_pool_floats", x.n, x.h * x.w, x.c_p, x.c))
+    buf = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
+    nv.call("ic2_global_avg_pool", nv.ptr(x.t), nv.dtype_code(x.t.dtype), x.n, x.h * x.w, x.c_p, x.c, nv.ptr(buf),
+            stream)
+    return buf[: x.n * x.c].view(x.n, x.c)
+
+
+def _linear(lin: nn.Linear, x, stream, act=False, slope=0.2):
+    n = x.shape[0]
+    y = torch.empty([n, lin.out_features], dtype=torch.float32, device=x.device)
+    nv.call("ic2_fc", nv.ptr(x), x.shape[1], nv.ptr(lin.weight), nv.ptr(lin.bias), nv.ptr(y), n, lin.in_features,
+            lin.out_features, 1.0, 1.0, nv.ACT_LRELU if act else nv.ACT_LINEAR, float(slope), 1.0, stream)
+    return y
+
+
+def _to_nhwc(x, dt, stream, c_p=None):
+    n, c, h, w = x.shape
+    c_p = nv.pad32(c) if c_p is None else c_p
+    out = torch.empty([n, h, w, c_p], dtype=dt, device=x.device)
+    nv.call("ic2_nchw_to_nhwc", nv.ptr(x), nv.ptr(out), nv.dtype_code(dt), n, c, h, w, c_p, None, stream)
+    return _Act(out, c)
+
+
+def _to_nchw(x: _Act, stream):
+    y = torch.empty([x.n, x.c, x.h, x.w], dtype=torch.float32, device=x.t.device)
+    nv.call("ic2_nhwc_to_nchw", nv.ptr(x.t), nv.dtype_code(x.t.dtype), nv.ptr(y), x.n, x.c, x.h, x.w, x.c_p, stream)
+    return y
+
+
+def _check_input(x):
+    x = x.to(torch.float32).contiguous()
+    nv.require_gpu(x)
+    return x
+
+
+# ================================================================================================
+class HVAE_VGG_Encoder(nn.Module):
+    """Full VGG-style HVAE encoder (ref ``stylegan3_hvae_full.py:29-167``)."""
+
+    def __init__(self, img_resolution=1024, img_channels=3, w_dim=512, num_ws=16, block_split=(5, 12),
+                 channel_base=32768, channel_max=512, use_fp16=False, precision="fp32"):
+        super().__init__()
+        self.img_resolution = img_resolution
+        self.img_channels = img_channels
+        self.w_dim = w_dim
+        self.num_ws = num_ws
+        self.block_split = block_split
+        self.use_fp16 = use_fp16
+        self.precision = precision
+        nv.torch_dtype(precision)
+        self.num_layers = int(np.log2(img_resolution))
+        channels = {}
+        for res in range(self.num_layers + 1):
+            channels[res] = min(channel_max, channel_base // (2 ** (self.num_layers - res)))
+        self.from_rgb = nn.Conv2d(img_channels, channels[0], kernel_size=3, padding=1)
+        self.blocks = nn.ModuleList()
+        for i in range(self.num_layers):
+            in_channels = channels[i]
+            out_channels = channels[i + 1] if i < self.num_layers - 1 else channels[i]
+            self.blocks.append(VGGBlock(in_channels, out_channels))
+        self.hierarchy_blocks = {"fine": 1, "medium": 4, "global": self.num_layers - 1}
+        self.num_ws_global = block_split[0]
+        self.num_ws_medium = block_split[1] - block_split[0]
+        self.num_ws_fine = num_ws - block_split[1]
+        self.global_projector = HierarchyProjector(channels[self.hierarchy_blocks["global"]], w_dim, self.num_ws_global)
+        self.medium_projector = HierarchyProjector(channels[self.hierarchy_blocks["medium"]], w_dim, self.num_ws_medium)
+        self.fine_projector = HierarchyProjector(channels[self.hierarchy_blocks["fine"]], w_dim, self.num_ws_fine)
+        self._cache = {}
+
+    def set_precision(self, precision):
+        nv.torch_dtype(precision)
+        self.precision = precision
+        return self
+
+    def features_nhwc(self, x, dt, stream):
+        """from_rgb + blocks with the reference's 1x1 break; returns {'fine','medium','global'} -> _Act."""
+        h = _to_nhwc(x, dt, stream)
+        h = _conv(self.from_rgb, h, dt, self._cache, stream)
+        feats = {}
+        for i, block in enumerate(self.blocks):
+            if h.h <= 1 or h.w <= 1:
+                break
+            h = block.run_nhwc(h, dt, self._cache, stream)
+            if i == self.hierarchy_blocks["fine"]:
+                feats["fine"] = h
+            elif i == self.hierarchy_blocks["medium"]:
+                feats["medium"] = h
+        feats["global"] = h
+        feats.setdefault("fine", h)
+        feats.setdefault("medium", h)
+        return feats
+
+    def forward(self, x):
+        """x [N, C, H, W] f32 in [-1, 1] -> (w_plus, means, logvars), each [N, num_ws, w_dim] f32."""
+        x = _check_input(x)
+        dt = nv.torch_dtype(self.precision)
+        stream = nv.stream_of(x)
+        feats = self.features_nhwc(x, dt, stream)
+        n = x.shape[0]
+        outs = [torch.empty([n, self.num_ws, self.w_dim], dtype=torch.float32, device=x.device) for _ in range(3)]
+        off = 0
+        for proj, key in ((self.global_projector, "global"), (self.medium_projector, "medium"),
+                          (self.fine_projector, "fine")):
+            proj.run_pooled(_gap(feats[key], stream), outs, off, self.num_ws, stream)
+            off += proj.num_ws
+        return tuple(outs)
+
+
+class VGGBlock(nn.Module):
+    """conv3x3 -> GroupNorm -> lrelu(0.2), twice, then AvgPool2d(2) (ref ``:170-191``)."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, kernel_size=3, padding=1)
+        self.norm1 = nn.GroupNorm(num_groups=min(32, out_channels), num_channels=out_channels)
+        self.norm2 = nn.GroupNorm(num_groups=min(32, out_channels), num_channels=out_channels)
+        self.pool = nn.AvgPool2d(kernel_size=2, stride=2)
+        self._cache = {}
+
+    def run_nhwc(self, x: _Act, dt, cache, stream):
+        y = _conv(self.conv1, x, dt, cache, stream)
+        h = _group_norm_lrelu(self.norm1, y, False, dt, stream)
+        y = _conv(self.conv2, h, dt, cache, stream)
+        pool = y.h > 1 and y.w > 1
+        return _group_norm_lrelu(self.norm2, y, pool, dt, stream)
+
+    def forward(self, x):
+        x = _check_input(x)
+        stream = nv.stream_of(x)
+        return _to_nchw(self.run_nhwc(_to_nhwc(x, torch.float32, stream), torch.float32, self._cache, stream), stream)
+
+
+class HierarchyProjector(nn.Module):
+    """GAP -> fc1 -> lrelu -> fc2 -> (mean, logvar) -> reparameterise (ref ``:194-247``)."""
+
+    def __init__(self, in_channels, w_dim, num_ws):
+        super().__init__()
+        self.w_dim = w_dim
+        self.num_ws = num_ws
+        self.in_channels = in_channels
+        self.pool = nn.AdaptiveAvgPool2d(1)
+        self.fc1 = nn.Linear(in_channels, 256)
+        self.act = nn.LeakyReLU(0.2)
+        self.fc2 = nn.Linear(256, num_ws * w_dim * 2)
+
+    def run_pooled(self, pooled, outs, off, ws_total, stream):
+        """pooled [N, C] f32 -> writes slots [off, off + num_ws) of (w, mean, logvar)."""
+        n, in_features = pooled.shape
+        if in_features != self.in_channels:
+            # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
+            self.fc1 = nn.Linear(in_features, 256).to(pooled.device)
+        h = _linear(self.fc1, pooled, stream, act=True, slope=self.act.negative_slope)
+        p = _linear(self.fc2, h, stream)
+        # torch.randn_like(std) on the device, in the reference's order (global, medium, fine)
+        eps = torch.randn([n, self.num_ws, self.w_dim], dtype=torch.float32, device=pooled.device)
+        w_out, m_out, lv_out = outs
+        nv.call("ic2_reparameterize", nv.ptr(p), nv.ptr(eps), n, self.num_ws, self.w_dim, ws_total, off, nv.ptr(w_out),
+                nv.ptr(m_out), nv.ptr(lv_out), stream)
+
+    def forward(self, x):
+        x = _check_input(x)
+        stream = nv.stream_of(x)
+        n = x.shape[0]
+        pooled = _gap(_to_nhwc(x, torch.float32, stream), stream).contiguous()
+        outs = [torch.empty([n, self.num_ws, self.w_dim], dtype=torch.float32, device=x.device) for _ in range(3)]
+        self.run_pooled(pooled, outs, 0, self.num_ws, stream)
+        return tuple(outs)
+
+
+# ================================================================================================
+def quantize_uniform(w, bits=8, return_indices=False):
+    """The compress() quantizer (ref ``:313-316``) as one bit-exact HIP kernel."""
+    w = w.to(torch.float32).contiguous()
+    nv.require_gpu(w)
+    q = torch.empty_like(w)
+    idx = torch.empty(w.shape, dtype=torch.int32, device=w.device) if return_indices else None
+    if w.data_ptr() % 16 or q.data_ptr() % 16:
+        raise RuntimeError("quantize_uniform needs 16-byte aligned tensors")
+    nv.call("ic2_quantize_uniform", nv.ptr(w), w.numel(), int(bits), nv.ptr(q), nv.ptr(idx), nv.stream_of(w))
+    return (q, idx) if return_indices else q
+
+
+def resize_bilinear(img, size):
+    """F.interpolate(img, size, mode='bilinear', align_corners=False) (ref ``:277-279``)."""
+    img = img.to(torch.float32).contiguous()
+    nv.require_gpu(img)
+    n, c, h, w = img.shape
+    oh, ow = size
+    out = torch.empty([n, c, oh, ow], dtype=torch.float32, device=img.device)
+    nv.call("ic2_resize_bilinear", nv.ptr(img), nv.ptr(out), n * c, h, w, oh, ow, nv.stream_of(img))
+    return out
+
+
+class StyleGAN3Compressor(nn.Module):
+    """Encoder + frozen StyleGAN3 generator codec (ref ``:250-380``)."""
+
+    def __init__(self, encoder, generator, training_resolution=None):
+        super().__init__()
+        self.encoder = encoder
+        self.generator = generator
+        self.training_resolution = training_resolution
+        for param in generator.parameters():
+            param.requires_grad = False
+
+    def forward(self, x, noise_mode="const"):
+        w_plus, _, _ = self.encoder(x)
+        img = self.generator.synthesis(w_plus, noise_mode=noise_mode)
+        if self.training_resolution is not None and img.shape[2] != x.shape[2]:
+            img = resize_bilinear(img, (x.shape[2], x.shape[3]))
+        return img, w_plus
+
+    def encode(self, x, deterministic=False):
+        w_plus, means, _ = self.encoder(x)
+        return means if deterministic else w_plus
+
+    def compress(self, x, quantization_bits=8, deterministic=True):
+        if deterministic:
+            _, w_plus, _ = self.encoder(x)
+        else:
+            w_plus, _, _ = self.encoder(x)
+        return quantize_uniform(w_plus, quantization_bits)
+
+    def decompress(self, w_plus, noise_mode="const"):
+        return self.generator.synthesis(w_plus, noise_mode=noise_mode)
+
+    def save_compressed(self, x, filename, quantization_bits=8, deterministic=True):
+        """Same .npz container as the reference (keys w, resolution, bits, orig_size, comp_size,
+        compression_ratio; ref ``:331-361``)."""
+        w_quantized = self.compress(x, quantization_bits, deterministic)
+        w_quantized_np = w_quantized.detach().cpu().numpy()
+        orig_size = x.numel() * 4
+        comp_size = w_quantized.numel() * (quantization_bits / 8)
+        np.savez_compressed(filename, w=w_quantized_np, resolution=x.shape[2:4], bits=quantization_bits,
+                            orig_size=orig_size, comp_size=comp_size, compression_ratio=orig_size / comp_size)
+        return orig_size, comp_size, orig_size / comp_size
+
+    def load_compressed(self, filename, noise_mode="const"):
+        data = np.load(filename)  # allow_pickle=False (default): plain arrays only
+        w_quantized = torch.tensor(data["w"]).to(next(self.generator.parameters()).device)
+        with torch.no_grad():
+            img = self.decompress(w_quantized, noise_mode=noise_mode)
+        return img, data["compression_ratio"]
+
+
+def save_tensor_as_image(tensor, filename):
+    """Tensor [C, H, W] in [-1, 1] -> PNG, exactly as the reference (no clamp; ref ``:923-932``)."""
+    img = tensor.detach().cpu().numpy()
+    img = ((img.transpose(1, 2, 0) + 1.0) * 127.5).astype(np.uint8)
+    Image.fromarray(img).save(filename)

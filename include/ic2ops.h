@@ -1,0 +1,187 @@
+/*
+ * ic2ops.h -- C ABI of libic2ops.so, the MI355X (gfx950) kernels behind the encode -> quantize ->
+ * synthesize path of yubster4525/image_compression_2 (reference snapshot mounted at /root/reference).
+ *
+ * Conventions (every entry point):
+ *   - all tensor pointers are DEVICE pointers owned by the caller (PyTorch's caching allocator);
+ *     nothing is allocated, freed or synchronised inside -> every call is hipGraph-capturable;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*; NULL = the legacy default stream);
+ *   - return IC2_OK (0) or an IC2_E_* code; ic2_last_error() returns the thread-local message;
+ *   - dtype codes: IC2_F32 = 0, IC2_BF16 = 1.  Activations on the synthesis path are NHWC with a
+ *     channel stride padded to a multiple of 32 ("c_p"); padded channels hold zeros.
+ *
+ * The reference has no native code and no C ABI: each entry point names the Python
+ * function of the reference (or of the un-vendored NVlabs/stylegan3 ops it calls) that it replaces.
+ */
+#ifndef IC2OPS_H_
+#define IC2OPS_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
+enum { IC2_F32 = 0, IC2_BF16 = 1 };
+enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
+enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1 };
+
+const char* ic2_last_error(void);
+int ic2_abi_version(void);
+
+/* ---------------------------------------------------------------- quantizers (HBM-bound) ---- */
+
+/* StyleGAN3Compressor.compress quantizer, stylegan3_hvae_full.py:313-316:
+ *   q = round(((w + 1) * 0.5) * S) / S * 2 - 1,  S = 2^bits - 1, fp32 in the written op order,
+ *   round half-to-even, no clamp.  idx_out (nullable) = the integer numerator round(((w+1)*0.5)*S). */
+int ic2_quantize_uniform(const float* w, int64_t n, int bits, float* q_out, int32_t* idx_out, void* stream);
+
+/* GumbelSoftmaxDiscretization.forward index path, gumbel_softmax_compression.py:93-118:
+ *   idx = argmin_k |z - codebook[k]| (exact fp32 distances, first index on ties).
+ *   zq_out (nullable) = codebook[idx] (the hard code, :258); hist_out (nullable, k counters, zeroed
+ *   by the caller) = code usage histogram (:121-123, feeds the perplexity :126-127). */
+int ic2_quantize_codebook_argmin(const float* z, int64_t n, const float* codebook, int k, int64_t* idx_out,
+                                 float* zq_out, uint32_t* hist_out, void* stream);
+
+/* GumbelSoftmaxCompressor.decompress lookup, gumbel_softmax_compression.py:255-259:
+ *   w = codebook[codes].  Out-of-range codes set *oob_flag (device int, zeroed by caller) and write 0. */
+int ic2_codebook_lookup(const int64_t* codes, int64_t n, const float* codebook, int k, float* w_out,
+                        int32_t* oob_flag, void* stream);
+
+/* GumbelSoftmaxDiscretization.forward, gumbel_softmax_compression.py:73-129, fused per latent:
+ *   y = (-|z - codebook| + gumbel) / tau;  soft = softmax(y);  ret = hard ? onehot(argmax) - soft + soft : soft;
+ *   disc_out = ret @ codebook;  idx_out (nullable) = exact argmin |z - c| (first index);
+ *   prob_sum_out (nullable, k floats, zeroed by caller) += column sums of ret (-> perplexity).
+ * tau = exp(*log_tau) when log_tau (device) is non-NULL, else `tau`.  Noise: gumbel_noise (device
+ * [n][k], nullable) or an in-kernel Philox4x32-10 stream keyed by (seed, offset + i*k + j). k <= 1024. */
+int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k, const float* log_tau,
+                                float tau, int hard, uint64_t seed, uint64_t offset, const float* gumbel_noise,
+                                float* disc_out, int64_t* idx_out, float* prob_sum_out, void* stream);
+
+/* ------------------------------------------- StyleGAN3 ops (torch_utils/ops, NVlabs/stylegan3) ---- */
+
+/* bias_act.bias_act(x, b, dim, act, alpha, gain, clamp) [SG3-public]; x viewed as [outer, c, inner],
+ * bias along c.  act: IC2_ACT_LINEAR / IC2_ACT_LRELU.  clamp < 0 = none. */
+int ic2_bias_act(const void* x, const float* b, void* y, int dtype, int64_t outer, int64_t c, int64_t inner,
+                 int act, float alpha, float gain, float clamp, void* stream);
+
+/* upfirdn2d.upfirdn2d(x, f, up, down, padding, flip_filter, gain) [SG3-public] on NCHW (nc planes).
+ * f (DEVICE pointer, f32): f_ndim = 1: separable f[f_w] (each pass scaled by sqrt(gain));
+ * f_ndim = 2: f[f_h][f_w] (scaled by gain).
+ * f == NULL: identity 1x1 filter.  Output size must be
+ *   out = (in*up + pad0 + pad1 - (taps-1)) / down  (ceil of the strided slice, as the ref computes). */
+int ic2_upfirdn2d(const void* x, void* y, int dtype, int64_t nc, int in_h, int in_w, int out_h, int out_w,
+                  const float* f, int f_ndim, int f_h, int f_w, int up_x, int up_y, int down_x, int down_y,
+                  int px0, int px1, int py0, int py1, int flip, float gain, void* stream);
+
+/* filtered_lrelu.filtered_lrelu(x, fu, fd, b, up, down, padding, gain, slope, clamp, flip_filter)
+ * [SG3-public] on NCHW, one fused launch: bias -> zero-insert up -> FIR fu (gain up^2) -> lrelu*gain ->
+ * clamp -> FIR fd -> keep every down-th.  fu/fd are 1-D separable taps in HOST memory (layer constants,
+ * passed by value in the kernel arguments; NULL = identity), b is a device pointer.
+ * Returns IC2_E_UNSUPPORTED for (up, down, taps) combinations without a fused instance; the caller
+ * then composes ic2_bias_act + ic2_upfirdn2d. */
+int ic2_filtered_lrelu(const void* x, void* y, int dtype, int64_t n, int64_t c, int in_h, int in_w, int out_h,
+                       int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps, const float* b,
+                       int up, int down, int px0, int px1, int py0, int py1, float gain, float slope,
+                       float clamp, int flip, void* stream);
+
+/* The synthesis-path variant of the same fused op: NHWC in/out with padded channel stride c_p,
+ * bias already folded into the producer (b may be NULL), and an optional per-(sample, channel)
+ * post_scale [n][c_p] (the NEXT layer's modulation, see ic2_modconv_prep) applied to the output. */
+int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_out, int n, int c_p, int in_h, int in_w,
+                    int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps, const float* b,
+                    int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
+                    int flip, const float* post_scale, void* stream);
+
+/* ----------------------------------------------------------------- modulated conv (MFMA) ---- */
+
+/* FullyConnectedLayer.forward [SG3-public] and nn.Linear (stylegan3_hvae_full.py:206-234):
+ *   y[n][o] = act((sum_i x[n*ldx + i] * w[o][i]) * w_gain + b[o] * b_gain) * act_gain   (fp32). */
+int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y, int n, int in_f, int out_f,
+           float w_gain, float b_gain, int act, float alpha, float act_gain, void* stream);
+
+/* Weight packing for the implicit GEMM: w[cout][cin][kh][kw] f32 -> w_out[cout_p][kh][kw][cin_p]
+ * (dtype) times `scale`, zero padded.  prenorm != 0 applies modulated_conv2d's w * rsqrt(mean(w^2,[1,2,3]))
+ * and writes wsq_out[cout][cin] = sum_k w_norm^2 (nullable).  Called once per weight version. */
+int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
+                    float scale, void* w_out, int dtype, float* wsq_out, void* stream);
+
+/* modulated_conv2d's modulation/demodulation coefficients [SG3-public], as the equivalent
+ * activation-scaling form y[n,o] = oscale[n,o] * sum_{i,k} w_norm[o,i,k] * (xscale[n,i] * x[n,i]):
+ *   demod:  s' = s * rsqrt(mean(s^2)) (batch-global), xscale = s',
+ *           oscale = input_gain * rsqrt(sum_i s'^2 * wsq[o][i] + 1e-8);
+ *   !demod: xscale = s * style_gain, oscale = input_gain.
+ * styles [n][cin] f32; xscale_out [n][cin_p]; oscale_out [n][cout_p]; scratch: 1 float. */
+int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int cout, int cin_p, int cout_p,
+                     int demod, float style_gain, float input_gain, float* xscale_out, float* oscale_out,
+                     float* scratch, void* stream);
+
+/* NHWC implicit-GEMM convolution on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32):
+ *   acc[n,p,o] = sum_{ky,kx,i} w[o][ky][kx][i] * x[n, p + (ky,kx) - pad, i]   (zero outside the image)
+ *   v = acc * (oscale ? oscale[n][o] : 1) + (bias ? bias[o] : 0);  if act: v = clamp(lrelu(v)*act_gain)
+ *   y = v * out_mul  -> NHWC [n][ho][wo][cout_p] (layout 0) or NCHW f32 [n][cout_valid][ho][wo] (layout 1).
+ * Replaces the grouped conv2d of modulated_conv2d [SG3-public] and nn.Conv2d of VGGBlock
+ * (stylegan3_hvae_full.py:175-176) / from_rgb (:62).  cin_p, cout_p multiples of 32. */
+int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
+                   int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
+                   const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
+                   float out_mul, int out_layout, void* stream);
+
+/* SynthesisInput.forward Fourier features [SG3-public]: t [n][4] = affine(w); per sample the
+ * rotation/translation of freqs/phases, the amplitude damping and sin(2*pi*(grid.f + phi)) * amp on a
+ * size x size grid -> x_out NHWC [n][size][size][c_p].  (The trailing @ W/sqrt(C) is an ic2_conv_igemm.) */
+int ic2_synth_input_features(const float* t, const float* freqs, const float* phases, const float* transform,
+                             int n, int c, int c_p, int size, float sampling_rate, float bandwidth, void* x_out,
+                             int dtype, void* stream);
+
+/* ------------------------------------------------------------------ encoder (HVAE_VGG) ---- */
+
+/* NCHW f32 -> NHWC (dtype) with channel stride c_p (zero padded), optionally times scale[n][c_p]
+ * (nullable; a modulated layer's input scaling); the encoder's input packing. */
+int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c, int h, int w, int c_p, const float* scale,
+                     void* stream);
+
+/* NHWC (dtype, channel stride c_p) -> NCHW f32 with c channels (layer-level API outputs). */
+int ic2_nhwc_to_nchw(const void* x, int dtype, float* y, int n, int c, int h, int w, int c_p, void* stream);
+
+/* nn.GroupNorm statistics (stylegan3_hvae_full.py:179-180; eps 1e-5): per (n, group) mean and
+ * rstd = 1/sqrt(var + eps) over (channels of the group) x H x W of the NHWC tensor y.
+ * stats_out [n][groups][2] f32, followed by scratch: ic2_group_norm_stats_floats() floats in total.
+ * Two-level deterministic reduction (no atomics). */
+int64_t ic2_group_norm_stats_floats(int n, int hw, int groups);
+int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c, int groups, float eps,
+                         float* stats_out, void* stream);
+
+/* GroupNorm apply + F.leaky_relu(0.2) (+ AvgPool2d(2,2) when pool != 0), VGGBlock.forward :183-191:
+ *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling). */
+int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p, int c,
+                      int groups, const float* stats, const float* gamma, const float* beta, float slope,
+                      int pool, void* stream);
+
+/* AdaptiveAvgPool2d(1) of HierarchyProjector (:218): out [n][c] f32 = mean over H x W (NHWC input);
+ * `out` is followed by scratch: ic2_global_avg_pool_floats() floats in total. */
+int64_t ic2_global_avg_pool_floats(int n, int hw, int c_p, int c);
+int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int c_p, int c, float* out, void* stream);
+
+/* HierarchyProjector tail (:237-245): params [n][num_ws][2*w_dim] -> mean, logvar (chunk), and
+ * w = mean + eps * exp(0.5*logvar) (eps nullable -> w = mean).  Outputs written at slot offset
+ * ws_off of [n][ws_total][w_dim] tensors (the torch.cat of :163-165 done in place). */
+int ic2_reparameterize(const float* params, const float* eps, int n, int num_ws, int w_dim, int ws_total,
+                       int ws_off, float* w_out, float* mean_out, float* logvar_out, void* stream);
+
+/* ------------------------------------------------------------------------------ metrics ---- */
+
+/* PSNR support (hvae_training.py:368-388 uint8 conversion): per image sum of squared differences of
+ * trunc(clamp(v*0.5+0.5,0,1)*255) between two NCHW f32 batches -> sse_out [n_img] (f64). */
+int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img, double* sse_out, void* stream);
+
+/* F.interpolate(mode='bilinear', align_corners=False, no antialias) of StyleGAN3Compressor.forward
+ * (stylegan3_hvae_full.py:277-279), NCHW f32. */
+int ic2_resize_bilinear(const float* x, float* y, int64_t nc, int h, int w, int oh, int ow, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IC2OPS_H_ */

@@ -1,0 +1,202 @@
+"""GPU parity of every libic2ops kernel against the CPU oracle (op level)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import image_compression_2_amd as ic2
+from image_compression_2_amd import _native as nv
+from image_compression_2_amd import gumbel_softmax_compression as gsc
+from image_compression_2_amd import metrics as icm
+from image_compression_2_amd import sg3_ops
+from image_compression_2_amd.stylegan3_hvae_full import _Act, _conv, _to_nhwc, _to_nchw
+from oracle import encoder as oe
+from oracle import metrics as om
+from oracle import sg3
+
+pytestmark = pytest.mark.gpu
+
+
+def _maxdiff(a, b):
+    return (a.detach().float().cpu() - b.detach().float().cpu()).abs().max().item()
+
+
+# ------------------------------------------------------------------ quantizers (bit-exact)
+@pytest.mark.parametrize("bits", [4, 8, 10])
+@pytest.mark.parametrize("tag", ["rand", "adv"])
+def test_quantize_uniform_bit_exact(cuda, golden_dir, bits, tag):
+    d = np.load(os.path.join(golden_dir, "quantizers.npz"))
+    w = torch.from_numpy(d[f"uniform_b{bits}_{tag}_w"]).to(cuda)
+    q, idx = ic2.quantize_uniform(w, bits, return_indices=True)
+    assert torch.equal(q.cpu(), torch.from_numpy(d[f"uniform_b{bits}_{tag}_q"]))
+    assert torch.equal(idx.cpu().long(), oe.uniform_indices(w.cpu(), bits))
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 4097])
+def test_quantize_uniform_ragged_sizes(cuda, n):
+    w = (torch.rand(n, generator=torch.Generator().manual_seed(n)) * 3 - 1.5)
+    q = ic2.quantize_uniform(w.to(cuda), 8)
+    assert torch.equal(q.cpu(), oe.quantize_uniform(w, 8))
+
+
+def test_codebook_argmin_bit_exact(cuda, golden_dir):
+    d = np.load(os.path.join(golden_dir, "quantizers.npz"))
+    z = torch.from_numpy(d["codebook_z"]).to(cuda)
+    cb = torch.from_numpy(d["codebook"]).to(cuda)
+    idx, hist = gsc.codebook_argmin(z, cb, hist=True)
+    ref = d["codebook_idx"]
+    assert np.array_equal(idx.cpu().numpy(), ref)
+    assert np.array_equal(hist.cpu().numpy().astype(np.int64), np.bincount(ref, minlength=256))
+
+
+def test_codebook_lookup_and_oob(cuda):
+    cb = oe.codebook().to(cuda)
+    codes = torch.randint(0, 256, (2, 16, 512), generator=torch.Generator().manual_seed(0))
+    w, flag = gsc.codebook_lookup(codes.to(cuda), cb)
+    assert torch.equal(w.cpu(), oe.codebook_lookup(codes))
+    assert flag.item() == 0
+    codes[0, 0, 0] = 300
+    _, flag = gsc.codebook_lookup(codes.to(cuda), cb)
+    assert flag.item() == 1
+
+
+def _gumbel_oracle(z, noise, tau, hard):
+    cb = oe.codebook()
+    logits = -torch.abs(z.reshape(-1, 1) - cb.reshape(1, -1))
+    y = (logits + noise) / tau
+    soft = y.softmax(1)
+    if hard:
+        index = soft.max(1, keepdim=True)[1]
+        ret = torch.zeros_like(logits).scatter_(1, index, 1.0) - soft + soft
+    else:
+        ret = soft
+    return ret @ cb, ret.mean(0), torch.argmin(torch.abs(z.reshape(-1, 1) - cb.reshape(1, -1)), 1)
+
+
+@pytest.mark.parametrize("hard", [False, True])
+def test_gumbel_softmax_with_given_noise(cuda, hard):
+    g = torch.Generator().manual_seed(3)
+    z = torch.rand(2, 4, 64, generator=g) * 2.2 - 1.1
+    noise = -torch.empty(z.numel(), 256).exponential_(generator=g).log()
+    disc_mod = ic2.GumbelSoftmaxDiscretization(64, 256, temperature=0.7).to(cuda)
+    disc, perp, idx = disc_mod(z.to(cuda), hard=hard, gumbel_noise=noise.to(cuda))
+    rdisc, ravg, ridx = _gumbel_oracle(z, noise, 0.7, hard)
+    assert torch.equal(idx.cpu(), ridx)
+    assert _maxdiff(disc.reshape(-1), rdisc.reshape(-1)) < 1e-5
+    rperp = torch.exp(-torch.sum(ravg * torch.log(ravg + 1e-10)))
+    assert abs(perp.item() - rperp.item()) < 1e-3 * rperp.item()
+
+
+def test_gumbel_softmax_generated_noise_statistics(cuda):
+    torch.manual_seed(0)
+    z = (torch.rand(4, 16, 512) * 2 - 1).to(cuda)
+    mod = ic2.GumbelSoftmaxDiscretization(512, 256).to(cuda).eval()
+    disc, perp, idx = mod(z, hard=True)
+    cb = mod.codebook
+    # hard straight-through output is a codebook value up to one rounding
+    nearest = cb[torch.argmin((disc.reshape(-1, 1) - cb.reshape(1, -1)).abs(), 1)]
+    assert (disc.reshape(-1) - nearest).abs().max().item() < 1e-6
+    # gumbel noise dominates the 2/255 logit gaps: most codes differ from argmin
+    frac_same = (nearest == cb[idx]).float().mean().item()
+    assert frac_same < 0.2
+    assert 100 < perp.item() <= 256
+
+
+# ------------------------------------------------------------------ SG3 ops vs oracle
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 2e-2)])
+def test_bias_act(cuda, dtype, tol):
+    x = torch.randn(2, 5, 7, 9)
+    b = torch.randn(5)
+    for act, kw in (("linear", {}), ("lrelu", dict(alpha=0.1, gain=1.7, clamp=1.5))):
+        y = sg3_ops.bias_act(x.to(cuda, dtype), b.to(cuda), act=act, **kw)
+        r = sg3.bias_act(x.to(dtype).float(), b, act=act, **kw)
+        assert _maxdiff(y, r) <= tol * (1 + r.abs().max().item())
+
+
+UFD_CASES = [
+    dict(up=2, down=1, padding=[5, 6, 5, 6], taps=12, flip=False),
+    dict(up=1, down=2, padding=0, taps=12, flip=False),
+    dict(up=4, down=2, padding=[-6, -9, -6, -9], taps=24, flip=True),
+    dict(up=2, down=2, padding=[1, 0, 2, 3], taps=5, flip=False),
+]
+
+
+@pytest.mark.parametrize("case", range(len(UFD_CASES)))
+@pytest.mark.parametrize("ndim", [1, 2])
+def test_upfirdn2d(cuda, case, ndim):
+    c = UFD_CASES[case]
+    g = torch.Generator().manual_seed(case)
+    x = torch.randn(2, 3, 20, 17, generator=g)
+    f = torch.rand(c["taps"], generator=g)
+    if ndim == 2:
+        f = torch.outer(f, torch.rand(c["taps"], generator=g))
+    kw = dict(up=c["up"], down=c["down"], padding=c["padding"], flip_filter=c["flip"], gain=c["up"] ** 2)
+    y = sg3_ops.upfirdn2d(x.to(cuda), f.to(cuda), **kw)
+    r = sg3.upfirdn2d(x, f, **kw)
+    assert y.shape == r.shape
+    assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item())
+
+
+FLR_CASES = [  # (up, down, taps_u, taps_d, padding, in size)
+    (2, 2, 12, 12, [9, 8, 9, 8], 38),
+    (4, 2, 24, 12, [-6, -9, -6, -9], 38),
+    (2, 2, 12, 12, [-11, -12, -11, -12], 40),
+    (1, 2, 1, 12, [3, 2, 3, 2], 21),   # no fused instance -> HIP composition
+]
+
+
+@pytest.mark.parametrize("case", range(len(FLR_CASES)))
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_filtered_lrelu_nchw(cuda, case, dtype):
+    up, down, tu, td, pad, s = FLR_CASES[case]
+    g = torch.Generator().manual_seed(10 + case)
+    x = torch.randn(2, 19, s, s, generator=g) * 3
+    b = torch.randn(19, generator=g)
+    fu = sg3.design_lowpass_filter(tu, 8.0, 4.0, 64) if tu > 1 else None
+    fd = sg3.design_lowpass_filter(td, 8.0, 4.0, 64) if td > 1 else None
+    kw = dict(up=up, down=down, padding=pad, gain=np.sqrt(2), slope=0.2, clamp=5.0)
+    y = sg3_ops.filtered_lrelu(x.to(cuda, dtype), None if fu is None else fu.to(cuda),
+                               None if fd is None else fd.to(cuda), b.to(cuda), **kw)
+    r = sg3.filtered_lrelu(x.to(dtype).double(), None if fu is None else fu.double(),
+                           None if fd is None else fd.double(), b.double(), **kw)
+    assert y.shape == r.shape and y.dtype == dtype
+    tol = 2e-5 if dtype == torch.float32 else 3e-2
+    assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
+
+
+# ------------------------------------------------------------------ implicit-GEMM conv (MFMA)
+@pytest.mark.parametrize("cin,cout,size,pad", [(3, 32, 19, 1), (64, 96, 12, 1), (181, 128, 9, 2), (512, 512, 6, 2)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_igemm(cuda, cin, cout, size, pad, dtype):
+    g = torch.Generator().manual_seed(cin + cout)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=pad)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+    x = torch.randn(3, cin, size, size, generator=g)
+    convg = conv.to(cuda)
+    stream = nv.stream_of(x.to(cuda))
+    y = _to_nchw(_conv(convg, _to_nhwc(x.to(cuda), dtype, stream), dtype, {}, stream), stream)
+    xr = x.to(dtype).float()
+    wr = conv.weight.detach().cpu().to(dtype).float()
+    r = F.conv2d(xr.double(), wr.double(), conv.bias.detach().cpu().double(), padding=pad)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
+
+
+# ------------------------------------------------------------------ metric / resize
+def test_uint8_sse_matches_reference_definition(cuda):
+    g = torch.Generator().manual_seed(4)
+    a = torch.rand(3, 3, 16, 16, generator=g) * 2.4 - 1.2
+    b = torch.rand(3, 3, 16, 16, generator=g) * 2 - 1
+    sse = icm.uint8_sse(a.to(cuda), b.to(cuda)).cpu().numpy()
+    assert np.array_equal(sse, om.sse_uint8(a, b))
+    assert icm.psnr(a.to(cuda), b.to(cuda)) == pytest.approx(om.psnr(a, b), abs=1e-9)
+
+
+def test_resize_bilinear(cuda):
+    x = torch.randn(2, 3, 64, 64)
+    y = ic2.resize_bilinear(x.to(cuda), (16, 16))
+    r = F.interpolate(x, size=(16, 16), mode="bilinear", align_corners=False)
+    assert _maxdiff(y, r) < 1e-5

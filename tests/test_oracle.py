@@ -1,0 +1,168 @@
+"""CPU: pin the oracle (oracle/) against the reference's golden vectors and known-answer tests."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import encoder as oe
+from oracle import metrics as om
+from oracle import sg3
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+# ------------------------------------------------------------------ quantizers vs reference goldens
+@pytest.mark.parametrize("bits", [4, 8, 10])
+@pytest.mark.parametrize("tag", ["rand", "adv"])
+def test_uniform_quantizer_matches_reference(golden_dir, bits, tag):
+    d = _load(golden_dir, "quantizers.npz")
+    w = torch.from_numpy(d[f"uniform_b{bits}_{tag}_w"])
+    q = oe.quantize_uniform(w, bits)
+    assert torch.equal(q, torch.from_numpy(d[f"uniform_b{bits}_{tag}_q"]))
+
+
+def test_codebook_argmin_matches_reference(golden_dir):
+    d = _load(golden_dir, "quantizers.npz")
+    assert np.array_equal(oe.codebook().numpy(), d["codebook"])
+    idx = oe.codebook_argmin(torch.from_numpy(d["codebook_z"]))
+    assert np.array_equal(idx.numpy(), d["codebook_idx"])
+
+
+def test_closed_form_is_not_the_reference(golden_dir):
+    """round((z+1)*127.5) disagrees with the reference's fp32 argmin on midpoints."""
+    d = _load(golden_dir, "quantizers.npz")
+    z = torch.from_numpy(d["codebook_z"]).reshape(-1).double()
+    closed = torch.round((z + 1) * 127.5).clamp(0, 255).long().numpy()
+    assert (closed != d["codebook_idx"]).sum() > 0
+
+
+# ------------------------------------------------------------------ encoder vs reference goldens
+def test_encoder_small_matches_reference(golden_dir):
+    d = _load(golden_dir, "encoder_small.npz")
+    sd = {k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("sd/")}
+    x = torch.from_numpy(d["x"])
+    means, lv, wp = (torch.from_numpy(d[k]) for k in ("means", "logvars", "w_plus"))
+    fc1 = (torch.from_numpy(d["fine_fc1_weight"]), torch.from_numpy(d["fine_fc1_bias"]))
+    eps_all = (wp - means) / torch.exp(0.5 * lv)
+    eps = {"global": eps_all[:, :5], "medium": eps_all[:, 5:12], "fine": eps_all[:, 12:]}
+    w, m, l = oe.encoder_forward(sd, x, w_dim=32, fine_fc1=fc1, eps=eps)
+    assert torch.equal(m, means)
+    assert torch.equal(l, lv)
+    assert torch.allclose(w, wp, atol=1e-6)
+    assert torch.equal(oe.quantize_uniform(m, 8), torch.from_numpy(d["compress_q8"]))
+
+
+def test_reference_containers_readable(golden_dir):
+    """The reference's own .npz containers load with allow_pickle=False and carry the documented keys."""
+    u = np.load(os.path.join(golden_dir, "ref_uniform_container.npz"))
+    assert set(u.files) == {"w", "resolution", "bits", "orig_size", "comp_size", "compression_ratio"}
+    assert u["w"].dtype == np.float32 and u["w"].shape == (1, 16, 32)
+    c = np.load(os.path.join(golden_dir, "ref_codebook_container.npz"))
+    assert set(c.files) == {"codes", "n_embeddings", "resolution", "orig_size", "comp_size", "compression_ratio"}
+    assert c["codes"].dtype == np.int64
+    assert float(u["compression_ratio"]) == 24.0
+
+
+# ------------------------------------------------------------------ SG3 restatement known answers
+def test_layer_names_match_published_1024():
+    _, layers = sg3.layer_table(1024)
+    names = [L["name"] for L in layers]
+    assert names == ["L0_36_512", "L1_36_512", "L2_52_512", "L3_52_512", "L4_84_512", "L5_148_512", "L6_148_512",
+                     "L7_276_323", "L8_276_203", "L9_532_128", "L10_1044_81", "L11_1044_51", "L12_1044_32",
+                     "L13_1024_32", "L14_1024_3"]
+
+
+def test_layer_table_256():
+    _, layers = sg3.layer_table(256)
+    assert [L["name"] for L in layers][-3:] == ["L12_276_128", "L13_256_128", "L14_256_3"]
+    for L in layers[:-1]:
+        oh, ow = sg3.filtered_lrelu_out_size(L["in_size"] + L["conv_kernel"] - 1, L["in_size"] + L["conv_kernel"] - 1,
+                                             L["up_taps"], L["down_taps"], L["up"], L["down"], L["padding"])
+        assert oh == ow == L["out_size"]
+
+
+def test_firwin_taps_symmetric_unity_dc():
+    _, layers = sg3.layer_table(256)
+    for L in layers[:-1]:
+        for f in (L["up_filter"], L["down_filter"]):
+            a = f.numpy().astype(np.float64)
+            assert np.allclose(a, a[::-1], atol=1e-7)
+            assert abs(a.sum() - 1.0) < 1e-6
+
+
+def test_upfirdn2d_impulse_returns_flipped_scaled_filter():
+    f = torch.tensor([1.0, 2.0, 3.0, 5.0])
+    x = torch.zeros(1, 1, 7, 7, dtype=torch.float64)
+    x[0, 0, 3, 3] = 1
+    y = sg3.upfirdn2d(x, f.double(), padding=3, gain=4.0)
+    # correlation with the flipped filter = convolution: the impulse reproduces f (times sqrt(gain) per axis)
+    expect = torch.outer(f, f).double() * 4.0
+    assert torch.allclose(y[0, 0, 3:7, 3:7], expect) or torch.allclose(y[0, 0, 2:6, 2:6], expect)
+
+
+def test_upfirdn2d_up_down_identity():
+    x = torch.randn(2, 3, 9, 11, dtype=torch.float64)
+    y = sg3.upfirdn2d(sg3.upfirdn2d(x, None, up=2), None, down=2)
+    assert torch.equal(x, y)
+
+
+def test_filtered_lrelu_is_the_four_op_composition():
+    torch.manual_seed(0)
+    x = torch.randn(2, 4, 12, 12, dtype=torch.float64)
+    b = torch.randn(4, dtype=torch.float64)
+    fu = sg3.design_lowpass_filter(12, 4.0, 3.0, 32).double()
+    fd = sg3.design_lowpass_filter(12, 4.0, 3.0, 32).double()
+    y = sg3.filtered_lrelu(x, fu, fd, b, up=2, down=2, padding=[9, 8, 9, 8], clamp=256)
+    t = x + b.view(1, -1, 1, 1)
+    t = sg3.upfirdn2d(t, fu, up=2, padding=[9, 8, 9, 8], gain=4)
+    t = F.leaky_relu(t, 0.2) * math.sqrt(2)
+    t = t.clamp(-256, 256)
+    t = sg3.upfirdn2d(t, fd, down=2)
+    assert torch.allclose(y, t)
+
+
+def test_modconv_grouped_equals_activation_scaling_form():
+    torch.manual_seed(1)
+    n, ci, co = 3, 8, 6
+    x = torch.randn(n, ci, 7, 7, dtype=torch.float64)
+    w = torch.randn(co, ci, 3, 3, dtype=torch.float64)
+    s = torch.randn(n, ci, dtype=torch.float64) + 1
+    y = sg3.modulated_conv2d(x, w, s, demodulate=True, padding=2, input_gain=0.7)
+    wn = w * w.square().mean([1, 2, 3], keepdim=True).rsqrt()
+    sn = s * s.square().mean().rsqrt()
+    d = ((sn.square() @ wn.square().sum([2, 3]).t()) + 1e-8).rsqrt()  # [n, co]
+    y2 = F.conv2d(x * sn.view(n, ci, 1, 1), wn, padding=2) * d.view(n, co, 1, 1) * 0.7
+    assert torch.allclose(y, y2, rtol=1e-12, atol=1e-12)
+
+
+def test_modconv_batch_prenorm_cancels_under_demod():
+    """The batch-global s * rsqrt(mean(s^2)) cancels under demodulation up to the 1e-8 epsilon, so
+    sharding the batch changes only rounding."""
+    torch.manual_seed(2)
+    x = torch.randn(4, 8, 6, 6, dtype=torch.float64)
+    w = torch.randn(5, 8, 3, 3, dtype=torch.float64)
+    s = torch.randn(4, 8, dtype=torch.float64)
+    full = sg3.modulated_conv2d(x, w, s, padding=2)
+    half = torch.cat([sg3.modulated_conv2d(x[:2], w, s[:2], padding=2), sg3.modulated_conv2d(x[2:], w, s[2:], padding=2)])
+    assert torch.allclose(full, half, rtol=1e-6, atol=1e-6)
+
+
+def test_synthesis_oracle_runs_small():
+    sd = sg3.init_params(256, seed=3)
+    ws = torch.randn(1, 16, 512) * 0.5
+    img = sg3.synthesis_forward(sd, 256, ws)
+    assert img.shape == (1, 3, 256, 256) and torch.isfinite(img).all()
+
+
+def test_psnr_definition():
+    a = torch.zeros(1, 3, 4, 4)
+    b = torch.zeros(1, 3, 4, 4)
+    b[0, 0, 0, 0] = 2 / 255.0 * 2  # 2 uint8 levels at one pixel (from 127 -> 129 after truncation)
+    ua, ub = om.to_uint8(a), om.to_uint8(b)
+    mse = ((ua.astype(float) - ub.astype(float)) ** 2).mean()
+    assert om.psnr(a, b) == pytest.approx(10 * math.log10(255 ** 2 / mse))
