@@ -68,4 +68,9 @@ __device__ __forceinline__ float lrelu_gain_clamp(float v, float slope, float ga
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// A zeroed 64-byte line in the code object: out-of-image loads read it instead of branching around
+// the load (a per-load branch makes hipcc wait vmcnt(0) per element -> serialised round trips).
+static __device__ __attribute__((aligned(64))) uint32_t g_zero_line[16] = {0};
+__device__ __forceinline__ const void* zero_line() { return g_zero_line; }
+
 }  // namespace ic2

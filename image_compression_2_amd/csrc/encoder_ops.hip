@@ -49,42 +49,53 @@ constexpr int GN_CHUNK_PIX = 256;
 template <typename T>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y, int hw, int c_p, int c, int groups,
                                                          int nchunks, double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) double sred[];  // [2][256]
+  // threads own channels (coalesced NHWC reads): thread t -> channel t % CT (+ k*256 when c_p > 256),
+  // pixel phase t / CT; per-thread fp32 sums over <= 256 pixels, then a fixed-order f64 group reduction
+  extern __shared__ __attribute__((aligned(16))) double sred[];  // [2][max(256, c_p)]
   const int chunk = blockIdx.x % nchunks;
   const int nn = blockIdx.x / nchunks;
   const int cpg = c / groups;
   const int p0 = chunk * GN_CHUNK_PIX;
   const int p1 = min(hw, p0 + GN_CHUNK_PIX);
   const T* yb = y + (int64_t)nn * hw * c_p;
-  double* sum = sred;
-  double* sq = sred + 256;
-  for (int g = 0; g < groups; ++g) {
-    // elements of group g in this chunk: (p1 - p0) * cpg, channel fastest
-    const int cnt = (p1 - p0) * cpg;
-    float s = 0.f, q = 0.f;
-    for (int e = threadIdx.x; e < cnt; e += 256) {
-      const int p = p0 + e / cpg;
-      const int ch = g * cpg + e % cpg;
-      const float v = ld(yb + (int64_t)p * c_p + ch);
-      s += v;
-      q += v * v;
-    }
-    sum[threadIdx.x] = s;
-    sq[threadIdx.x] = q;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-      if (threadIdx.x < off) {
-        sum[threadIdx.x] += sum[threadIdx.x + off];
-        sq[threadIdx.x] += sq[threadIdx.x + off];
+  const int CT = c_p < 256 ? c_p : 256;  // channels covered per pass
+  const int PS = 256 / CT;               // pixel phases
+  const int ch0 = threadIdx.x % CT;
+  const int pp = threadIdx.x / CT;
+  const int nslots = c_p < 256 ? 256 : c_p;
+  double* ssum = sred;
+  double* ssq = sred + nslots;
+  if (pp < PS) {
+    for (int cc = ch0; cc < c_p; cc += 256) {
+      float s = 0.f, q = 0.f;
+      for (int p = p0 + pp; p < p1; p += PS) {
+        const float v = ld(yb + (int64_t)p * c_p + cc);
+        s += v;
+        q += v * v;
       }
-      __syncthreads();
+      const int slot = c_p < 256 ? threadIdx.x : cc;
+      ssum[slot] = s;
+      ssq[slot] = q;
     }
-    if (threadIdx.x == 0) {
-      double* o = part + (((int64_t)nn * groups + g) * nchunks + chunk) * 2;
-      o[0] = sum[0];
-      o[1] = sq[0];
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < groups; g += 256) {
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < cpg; ++k) {
+      const int cc = g * cpg + k;
+      if (c_p < 256) {
+        for (int ph = 0; ph < PS; ++ph) {
+          s += ssum[ph * CT + cc];
+          q += ssq[ph * CT + cc];
+        }
+      } else {
+        s += ssum[cc];
+        q += ssq[cc];
+      }
     }
-    __syncthreads();
+    double* o = part + (((int64_t)nn * groups + g) * nchunks + chunk) * 2;
+    o[0] = s;
+    o[1] = q;
   }
 }
 
@@ -302,7 +313,7 @@ extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int
   const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
   double* part = reinterpret_cast<double*>(stats_out + stats_floats);
   hipStream_t s = as_stream(stream);
-  const size_t lds = 2 * 256 * sizeof(double);
+  const size_t lds = 2 * (size_t)(c_p < 256 ? 256 : c_p) * sizeof(double);
   if (dtype == IC2_F32)
     hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(n * nchunks), dim3(256), lds, s, (const float*)y, hw, c_p, c,
                        groups, nchunks, part);

@@ -15,6 +15,8 @@
 // padding (crop) is exact: input samples outside [0, L) are zero, as in the reference.
 #include "common.h"
 
+#include <type_traits>
+
 namespace ic2 {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -44,38 +46,58 @@ struct FlrGeom {
   static constexpr int NINXP = NINX | 1;               // odd row pitch: conflict-free ds_read_b64
 };
 
-template <typename T> __device__ __forceinline__ f2v load2(const T* p, int64_t sc, bool pair, bool second_ok);
-template <> __device__ __forceinline__ f2v load2<float>(const float* p, int64_t sc, bool pair, bool ok2) {
-  if (pair) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    return f2v{v.x, v.y};
-  }
-  return f2v{p[0], ok2 ? p[sc] : 0.f};
+// Branch-free pair access: an out-of-range sample reads the code object's zero line and is then
+// masked, so no load sits behind a branch (hipcc would otherwise wait vmcnt(0) per element).
+template <typename T, bool CHLAST>
+__device__ __forceinline__ f2v load2(const T* p, int64_t sc, bool ok, bool ok2);
+template <> __device__ __forceinline__ f2v load2<float, true>(const float* p, int64_t, bool ok, bool) {
+  const float2 v = *reinterpret_cast<const float2*>(ok ? (const void*)p : zero_line());
+  return f2v{v.x, v.y};
 }
-template <> __device__ __forceinline__ f2v load2<bf16_t>(const bf16_t* p, int64_t sc, bool pair, bool ok2) {
-  if (pair) {
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+template <> __device__ __forceinline__ f2v load2<bf16_t, true>(const bf16_t* p, int64_t, bool ok, bool) {
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(ok ? (const void*)p : zero_line());
+  return f2v{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+}
+template <> __device__ __forceinline__ f2v load2<float, false>(const float* p, int64_t sc, bool ok, bool ok2) {
+  const float a = *reinterpret_cast<const float*>(ok ? (const void*)p : zero_line());
+  const float b = *reinterpret_cast<const float*>(ok && ok2 ? (const void*)(p + sc) : zero_line());
+  return f2v{a, b};
+}
+template <> __device__ __forceinline__ f2v load2<bf16_t, false>(const bf16_t* p, int64_t sc, bool ok, bool ok2) {
+  const bf16_t a = *reinterpret_cast<const bf16_t*>(ok ? (const void*)p : zero_line());
+  const bf16_t b = *reinterpret_cast<const bf16_t*>(ok && ok2 ? (const void*)(p + sc) : zero_line());
+  return f2v{bf2f(a), bf2f(b)};
+}
+template <typename T, bool CHLAST> __device__ __forceinline__ void store2(T* p, int64_t sc, bool ok2, f2v v);
+template <> __device__ __forceinline__ void store2<float, true>(float* p, int64_t, bool, f2v v) {
+  *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y);
+}
+template <> __device__ __forceinline__ void store2<bf16_t, true>(bf16_t* p, int64_t, bool, f2v v) {
+  *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+}
+template <> __device__ __forceinline__ void store2<float, false>(float* p, int64_t sc, bool ok2, f2v v) {
+  p[0] = v.x;
+  if (ok2) p[sc] = v.y;
+}
+template <> __device__ __forceinline__ void store2<bf16_t, false>(bf16_t* p, int64_t sc, bool ok2, f2v v) {
+  p[0] = f2bf(v.x);
+  if (ok2) p[sc] = f2bf(v.y);
+}
+
+// LDS storage of the up-sampled grid: fp32 pairs (parity path) or packed bf16 pairs (bf16 path:
+// halves the LDS footprint -> twice the resident workgroups; one extra rounding of the vertically
+// up-sampled input, below the bf16 rounding of the output itself).
+template <typename LT> struct LdsPair;
+template <> struct LdsPair<f2v> {
+  __device__ static __forceinline__ f2v pack(f2v v) { return v; }
+  __device__ static __forceinline__ f2v unpack(f2v v) { return v; }
+};
+template <> struct LdsPair<uint32_t> {
+  __device__ static __forceinline__ uint32_t pack(f2v v) { return (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16); }
+  __device__ static __forceinline__ f2v unpack(uint32_t v) {
     return f2v{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
   }
-  return f2v{bf2f(p[0]), ok2 ? bf2f(p[sc]) : 0.f};
-}
-template <typename T> __device__ __forceinline__ void store2(T* p, int64_t sc, bool pair, bool ok2, f2v v);
-template <> __device__ __forceinline__ void store2<float>(float* p, int64_t sc, bool pair, bool ok2, f2v v) {
-  if (pair) {
-    *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y);
-  } else {
-    p[0] = v.x;
-    if (ok2) p[sc] = v.y;
-  }
-}
-template <> __device__ __forceinline__ void store2<bf16_t>(bf16_t* p, int64_t sc, bool pair, bool ok2, f2v v) {
-  if (pair) {
-    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-  } else {
-    p[0] = f2bf(v.x);
-    if (ok2) p[sc] = f2bf(v.y);
-  }
-}
+};
 
 __device__ __forceinline__ f2v act2(f2v a, float slope, float gain, float clamp) {
   f2v r;
@@ -91,9 +113,11 @@ constexpr int FLR_NCG = FLR_CPB / 2;     // channel pairs
 template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DELTA, int TOY, int TOX>
 __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
   using G = FlrGeom<U, D, TU, TD, TOY, TOX>;
+  using LT = typename std::conditional<std::is_same<TI, bf16_t>::value, uint32_t, f2v>::type;
+  using LP = LdsPair<LT>;
   constexpr int RAY = G::RAY, RAX = G::RAX, NINY = G::NINY, NINX = G::NINX, NINXP = G::NINXP;
   constexpr int NCG = FLR_NCG;
-  __shared__ __attribute__((aligned(16))) f2v buf[RAY * NINXP * NCG];
+  __shared__ __attribute__((aligned(16))) LT buf[RAY * NINXP * NCG];
 
   int bid = blockIdx.x;
   const int cb = bid % a.cblocks;
@@ -121,17 +145,18 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     const bool col_ok = (unsigned)ix < (unsigned)a.in_w && c < a.c;
     const bool ok2 = c + 1 < a.c;
     f2v bsum = f2v{0.f, 0.f};
-    if (a.bias && col_ok) bsum = f2v{a.bias[c], ok2 ? a.bias[c + 1] : 0.f};
+    if (a.bias) {
+      const int cc = col_ok ? c : 0;
+      bsum = f2v{a.bias[cc], ok2 ? a.bias[cc + 1] : 0.f};
+    }
+    const TI* pcol = xin + (int64_t)ix * a.xsx + (int64_t)c * a.xsc;
     f2v in[NINY];
 #pragma unroll
     for (int j = 0; j < NINY; ++j) {
       const int iy = sy0 + j;
-      if (col_ok && (unsigned)iy < (unsigned)a.in_h) {
-        const TI* p = xin + (int64_t)iy * a.xsy + (int64_t)ix * a.xsx + (int64_t)c * a.xsc;
-        in[j] = load2<TI>(p, a.xsc, CHLAST && ok2, ok2) + bsum;
-      } else {
-        in[j] = f2v{0.f, 0.f};
-      }
+      const bool ok = col_ok && (unsigned)iy < (unsigned)a.in_h;
+      const f2v v = load2<TI, CHLAST>(pcol + (int64_t)iy * a.xsy, a.xsc, ok, ok2) + bsum;
+      in[j] = ok ? v : f2v{0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < RAY; ++i) {
@@ -141,7 +166,7 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
         const int t = U * j + DELTA - i;
         if (t >= 0 && t < TU) acc += a.gu[t] * in[j];
       }
-      buf[(i * NINXP + xs) * NCG + cg] = acc;
+      buf[(i * NINXP + xs) * NCG + cg] = LP::pack(acc);
     }
   }
   __syncthreads();
@@ -152,7 +177,7 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     const int cg = item - i * NCG;
     f2v in[NINX];
 #pragma unroll
-    for (int j = 0; j < NINX; ++j) in[j] = buf[(i * NINXP + j) * NCG + cg];
+    for (int j = 0; j < NINX; ++j) in[j] = LP::unpack(buf[(i * NINXP + j) * NCG + cg]);
     f2v d[TOX];
 #pragma unroll
     for (int o = 0; o < TOX; ++o) d[o] = f2v{0.f, 0.f};
@@ -172,7 +197,7 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
       }
     }
 #pragma unroll
-    for (int o = 0; o < TOX; ++o) buf[(i * NINXP + o) * NCG + cg] = d[o];
+    for (int o = 0; o < TOX; ++o) buf[(i * NINXP + o) * NCG + cg] = LP::pack(d[o]);
   }
   __syncthreads();
 
@@ -189,7 +214,7 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     for (int r = 0; r < TOY; ++r) o[r] = f2v{0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < RAY; ++i) {
-      const f2v v = buf[(i * NINXP + ox) * NCG + cg];
+      const f2v v = LP::unpack(buf[(i * NINXP + ox) * NCG + cg]);
 #pragma unroll
       for (int r = 0; r < TOY; ++r) {
         const int t = i - r * D;
@@ -198,13 +223,11 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     }
     f2v ps = f2v{1.f, 1.f};
     if (a.post_scale) ps = f2v{a.post_scale[(int64_t)n * a.c_p + c], ok2 ? a.post_scale[(int64_t)n * a.c_p + c + 1] : 0.f};
+    TO* pout = yout + (int64_t)gx * a.ysx + (int64_t)c * a.ysc;
 #pragma unroll
     for (int r = 0; r < TOY; ++r) {
       const int gy = oy0 + r;
-      if (gy < a.out_h) {
-        TO* p = yout + (int64_t)gy * a.ysy + (int64_t)gx * a.ysx + (int64_t)c * a.ysc;
-        store2<TO>(p, a.ysc, CHLAST && ok2, ok2, o[r] * ps);
-      }
+      if (gy < a.out_h) store2<TO, CHLAST>(pout + (int64_t)gy * a.ysy, a.ysc, ok2, o[r] * ps);
     }
   }
 }

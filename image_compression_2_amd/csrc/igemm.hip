@@ -12,8 +12,9 @@
 // Tile 128(o) x 128(p) x 32(k), 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 MFMA tiles.
 //   bf16: v_mfma_f32_16x16x32_bf16 (one MFMA per 16x16 tile per chunk)
 //   f32 : v_mfma_f32_16x16x4_f32   (exact fp32 FMA chain; 8 MFMAs per tile per chunk)
-// LDS: double-buffered W and X tiles, rows XOR-swizzled per 16-B chunk (bank-conflict-free reads
-// for bf16, 2-way for f32); register-staged global loads of the next chunk overlap the MFMAs.
+// LDS: double-buffered W and X tiles filled by LDS-DMA (global_load_lds_dwordx4) one chunk ahead of
+// the MFMAs; rows XOR-swizzled per 16-B chunk via the source address (conflict-free fragment reads
+// for bf16, 2-way for f32).
 #include "common.h"
 
 namespace ic2 {
@@ -46,6 +47,7 @@ struct IgTraits {
   static constexpr int NLD = 128 * CPR / 256;    // chunks per thread per operand (2 / 4)
   static constexpr int TILEB = 128 * ROWB;       // bytes per operand tile
   static constexpr int RSTEP = 256 / CPR;        // row step between a thread's chunks
+  static constexpr int NSTAGE = BF16 ? 4 : 2;    // LDS ring depth (chunks in flight = NSTAGE - 1)
   __device__ static __forceinline__ int swz(int row) { return BF16 ? ((row >> 1) & 3) : ((row >> 1) & 7); }
   __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
 };
@@ -54,7 +56,8 @@ template <bool BF16>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
   using TR = IgTraits<BF16>;
   constexpr int CPR = TR::CPR, NLD = TR::NLD, EPC = TR::EPC, ESZ = TR::ESZ;
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TR::TILEB];
+  constexpr int NSTAGE = TR::NSTAGE;
+  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * 2 * TR::TILEB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -70,71 +73,63 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
   const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
   const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
 
-  // ---- per-thread load slots: rows r_j = tid / CPR + j * RSTEP, chunk ch = tid % CPR
-  const int ch = tid % CPR;
-  int x_nb[NLD], x_oy[NLD], x_ox[NLD];
-  bool x_ok[NLD];
-  bool w_ok[NLD];
-  int64_t w_base[NLD];
+  // ---- global -> LDS by LDS-DMA (global_load_lds_dwordx4): no register staging, so nothing can
+  // serialise the loads behind a wait.  Wave w, instruction k fills LDS bytes
+  // [(w*NI + k) * 1 KiB, +1 KiB) of an operand tile, lane l writing base + 16*l (lane-linear).  The
+  // bank swizzle therefore moves to the SOURCE: the lane that lands on physical 16-B slot p of row r
+  // fetches logical chunk p ^ swz(r); the fragment reads apply the same XOR.  Out-of-image pixels
+  // and padded output channels read the code object's zero line.
+  constexpr int NI = TR::TILEB / 1024 / 4;  // DMA instructions per wave per operand (2 / 4)
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  int x_nb[NI], x_oy[NI], x_ox[NI], x_ch[NI];
+  bool x_ok[NI];
+  int64_t w_off[NI];
+  bool w_ok[NI];
 #pragma unroll
-  for (int j = 0; j < NLD; ++j) {
-    const int row = tid / CPR + j * TR::RSTEP;
+  for (int k = 0; k < NI; ++k) {
+    const int off = (wid * NI + k) * 1024 + lane * 16;
+    const int row = off / TR::ROWB;
+    const int chl = ((off % TR::ROWB) >> 4) ^ TR::swz(row);
+    x_ch[k] = chl;
     const int m = m0 + row;
-    x_ok[j] = m < a.M;
-    const int mm = x_ok[j] ? m : 0;
+    x_ok[k] = m < a.M;
+    const int mm = x_ok[k] ? m : 0;
     const int hw = a.ho * a.wo;
     const int nn = mm / hw;
     const int rem = mm - nn * hw;
     const int oy = rem / a.wo;
-    x_nb[j] = nn * a.h;
-    x_oy[j] = oy - a.pad;
-    x_ox[j] = rem - oy * a.wo - a.pad;
+    x_nb[k] = nn * a.h;
+    x_oy[k] = oy - a.pad;
+    x_ox[k] = rem - oy * a.wo - a.pad;
     const int o = o0 + row;
-    w_ok[j] = o < a.cout_p;
-    w_base[j] = (int64_t)(w_ok[j] ? o : 0) * a.K * ESZ + ch * 16;
+    w_ok[k] = o < a.cout_p;
+    w_off[k] = (int64_t)(w_ok[k] ? o : 0) * a.K * ESZ + chl * 16;
   }
-
   const int CB = a.cin_p >> 5;
-  int q_cb = 0, q_kx = 0, q_ky = 0;  // decomposition of the chunk being loaded
 
-  uint4 xr[NLD], wr[NLD];
-  auto load_chunk = [&](int q) {
-#pragma unroll
-    for (int j = 0; j < NLD; ++j) {
-      const int iy = x_oy[j] + q_ky;
-      const int ix = x_ox[j] + q_kx;
-      const bool ok = x_ok[j] && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
-      if (ok) {
-        const int64_t e = ((int64_t)(x_nb[j] + iy) * a.w_ + ix) * a.cin_p + q_cb * 32 + ch * EPC;
-        xr[j] = *reinterpret_cast<const uint4*>(xg + e * ESZ);
-      } else {
-        xr[j] = make_uint4(0, 0, 0, 0);
-      }
-      if (w_ok[j]) {
-        wr[j] = *reinterpret_cast<const uint4*>(wg + w_base[j] + (int64_t)q * 32 * ESZ);
-      } else {
-        wr[j] = make_uint4(0, 0, 0, 0);
-      }
-    }
-    (void)q;
-    if (++q_cb == CB) {
-      q_cb = 0;
-      if (++q_kx == a.kw) {
-        q_kx = 0;
-        ++q_ky;
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-    char* wl = lds + buf * 2 * TR::TILEB;
-    char* xl = wl + TR::TILEB;
-#pragma unroll
-    for (int j = 0; j < NLD; ++j) {
-      const int row = tid / CPR + j * TR::RSTEP;
-      *reinterpret_cast<uint4*>(wl + TR::off(row, ch)) = wr[j];
-      *reinterpret_cast<uint4*>(xl + TR::off(row, ch)) = xr[j];
-    }
-  };
+#define IC2_IG_ISSUE(q_, buf_)                                                                                \
+  {                                                                                                          \
+    const int q__ = (q_);                                                                                    \
+    const int tap = q__ / CB;                                                                                \
+    const int cbk = q__ - tap * CB;                                                                          \
+    const int ky = tap / a.kw;                                                                               \
+    const int kx = tap - ky * a.kw;                                                                          \
+    char* wl_ = lds + (buf_) * 2 * TR::TILEB;                                                                \
+    char* xl_ = wl_ + TR::TILEB;                                                                             \
+    _Pragma("unroll") for (int k = 0; k < NI; ++k) {                                                         \
+      const int iy = x_oy[k] + ky;                                                                           \
+      const int ix = x_ox[k] + kx;                                                                           \
+      const bool ok = x_ok[k] && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;              \
+      const int64_t e = ((int64_t)(x_nb[k] + iy) * a.w_ + ix) * a.cin_p + cbk * 32 + x_ch[k] * EPC;          \
+      const void* xs = ok ? (const void*)(xg + e * ESZ) : zero_line();                                       \
+      const void* ws = w_ok[k] ? (const void*)(wg + w_off[k] + (int64_t)q__ * 32 * ESZ) : zero_line();       \
+      const int seg = (wid_u * NI + k) * 1024;                                                               \
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)xs,                     \
+                                       (__attribute__((address_space(3))) void*)(xl_ + seg), 16, 0, 0);      \
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ws,                     \
+                                       (__attribute__((address_space(3))) void*)(wl_ + seg), 16, 0, 0);      \
+    }                                                                                                        \
+  }
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -142,17 +137,26 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_chunk(0);
-  store_chunk(0);
-  __syncthreads();
+  // ring pipeline: chunks q+1 .. q+NSTAGE-2 stay in flight across the barrier (counted vmcnt, raw
+  // s_barrier -- __syncthreads() would drain every DMA with vmcnt(0))
+  constexpr int PER = 2 * NI;  // DMA instructions per wave per chunk
+#pragma unroll
+  for (int s_ = 0; s_ < NSTAGE - 1; ++s_) IC2_IG_ISSUE(s_ < a.nq ? s_ : a.nq - 1, s_);
 
   const int fr = lane & 15;
   const int fh = lane >> 4;
 
   for (int q = 0; q < a.nq; ++q) {
-    const int cur = q & 1;
-    const bool more = q + 1 < a.nq;
-    if (more) load_chunk(q + 1);
+    const int cur = q % NSTAGE;
+    if constexpr (NSTAGE == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // chunk q landed for every wave; chunk q-1 fully read
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int qn = q + NSTAGE - 1;
+      IC2_IG_ISSUE(qn < a.nq ? qn : a.nq - 1, qn % NSTAGE);  // refill the slot chunk q-1 used
+    }
+    __builtin_amdgcn_sched_barrier(0);
     const char* wl = lds + cur * 2 * TR::TILEB;
     const char* xl = wl + TR::TILEB;
     if constexpr (BF16) {
@@ -194,10 +198,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s >> 2][s & 3], bfr[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
     }
-    if (more) store_chunk(cur ^ 1);
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);  // every MFMA of this chunk before the next wait
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the redundant tail DMAs before exit
 
+#undef IC2_IG_ISSUE
   // ---- epilogue: lane holds C[o = base + 4*fh + r][p = base + fr]
   const int hw = a.ho * a.wo;
 #pragma unroll

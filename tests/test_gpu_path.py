@@ -189,6 +189,7 @@ def test_gumbel_compressor_round_trip(cuda, gen256):
     enc = ic2.HVAE_VGG_Encoder(img_resolution=1024).to(cuda)
     comp = ic2.GumbelSoftmaxCompressor(enc, gen256).to(cuda)
     x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(cuda)
+    torch.manual_seed(4)  # the fine fc1 is re-drawn from the CPU generator on every call (reference quirk)
     codes = comp.compress(x)
     assert codes.dtype == torch.int64 and codes.device.type == "cpu" and codes.shape == (2, 16, 512)
     torch.manual_seed(4)
