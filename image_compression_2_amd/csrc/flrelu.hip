@@ -15,6 +15,7 @@
 // padding (crop) is exact: input samples outside [0, L) are zero, as in the reference.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace ic2 {
@@ -32,7 +33,8 @@ struct FlrArgs {
   int in_h, in_w, out_h, out_w;
   int py0, px0;                 // leading padding
   int tiles_x, tiles_y, cblocks;
-  float gain, slope, clamp;
+  float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
+  float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
   float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
   float gd[12];  // flipped (unless flip_filter)
 };
@@ -99,19 +101,23 @@ template <> struct LdsPair<uint32_t> {
   }
 };
 
-__device__ __forceinline__ f2v act2(f2v a, float slope, float gain, float clamp) {
+// lrelu + clamp on a channel pair in 5 instructions: one packed multiply, two max (slope <= 1 makes
+// lrelu(v) = max(v, slope*v)) and two med3 clamps.  The gain is folded into the horizontal down taps
+// and the clamp bound divided by it: clamp(gain*lrelu(v), +-c) = gain * clamp(lrelu(v), +-c/gain).
+__device__ __forceinline__ f2v act2(f2v v, float slope, float lim) {
+  const f2v sv = v * slope;
   f2v r;
-  r.x = lrelu_gain_clamp(a.x, slope, gain, clamp);
-  r.y = lrelu_gain_clamp(a.y, slope, gain, clamp);
+  r.x = __builtin_amdgcn_fmed3f(fmaxf(v.x, sv.x), -lim, lim);
+  r.y = __builtin_amdgcn_fmed3f(fmaxf(v.y, sv.y), -lim, lim);
   return r;
 }
 
-constexpr int FLR_THREADS = 128;
-constexpr int FLR_CPB = 16;              // channels per workgroup
-constexpr int FLR_NCG = FLR_CPB / 2;     // channel pairs
+constexpr int FLR_S3 = 4;                // stage-3 row split (items = columns x pairs x FLR_S3)
 
-template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DELTA, int TOY, int TOX>
+template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DELTA, int TOY, int TOX, int FLR_CPB,
+          int FLR_THREADS>
 __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
+  constexpr int FLR_NCG = FLR_CPB / 2;  // channel pairs per workgroup
   using G = FlrGeom<U, D, TU, TD, TOY, TOX>;
   using LT = typename std::conditional<std::is_same<TI, bf16_t>::value, uint32_t, f2v>::type;
   using LP = LdsPair<LT>;
@@ -189,11 +195,11 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
         const int t = U * j + DELTA - k;
         if (t >= 0 && t < TU) v += a.gu[t] * in[j];
       }
-      v = act2(v, a.slope, a.gain, a.clamp);
+      v = act2(v, a.slope, a.lim);
 #pragma unroll
       for (int o = 0; o < TOX; ++o) {
         const int t = k - o * D;
-        if (t >= 0 && t < TD) d[o] += a.gd[t] * v;
+        if (t >= 0 && t < TD) d[o] += a.gdg[t] * v;
       }
     }
 #pragma unroll
@@ -201,23 +207,28 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
   }
   __syncthreads();
 
-  // ---------------- stage 3: vertical down-FIR per output column, store
-  for (int item = threadIdx.x; item < TOX * NCG; item += FLR_THREADS) {
-    const int ox = item / NCG;
-    const int cg = item - ox * NCG;
+  // ---------------- stage 3: vertical down-FIR per output column (FLR_S3 row groups), store
+  static_assert(TOY % FLR_S3 == 0, "TOY must split into FLR_S3 row groups");
+  constexpr int RG = TOY / FLR_S3;            // output rows per item
+  constexpr int RGI = (RG - 1) * D + TD;      // grid rows feeding them
+  for (int item = threadIdx.x; item < TOX * NCG * FLR_S3; item += FLR_THREADS) {
+    const int cg = item % NCG;
+    const int ox = (item / NCG) % TOX;
+    const int rg = item / (NCG * TOX);
     const int c = c0 + 2 * cg;
     const int gx = ox0 + ox;
     if (gx >= a.out_w || c >= a.c) continue;
     const bool ok2 = c + 1 < a.c;
-    f2v o[TOY];
+    f2v o[RG];
 #pragma unroll
-    for (int r = 0; r < TOY; ++r) o[r] = f2v{0.f, 0.f};
+    for (int r = 0; r < RG; ++r) o[r] = f2v{0.f, 0.f};
+    const int i0 = rg * RG * D;
 #pragma unroll
-    for (int i = 0; i < RAY; ++i) {
-      const f2v v = LP::unpack(buf[(i * NINXP + ox) * NCG + cg]);
+    for (int ii = 0; ii < RGI; ++ii) {
+      const f2v v = LP::unpack(buf[((i0 + ii) * NINXP + ox) * NCG + cg]);
 #pragma unroll
-      for (int r = 0; r < TOY; ++r) {
-        const int t = i - r * D;
+      for (int r = 0; r < RG; ++r) {
+        const int t = ii - r * D;
         if (t >= 0 && t < TD) o[r] += a.gd[t] * v;
       }
     }
@@ -225,8 +236,8 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     if (a.post_scale) ps = f2v{a.post_scale[(int64_t)n * a.c_p + c], ok2 ? a.post_scale[(int64_t)n * a.c_p + c + 1] : 0.f};
     TO* pout = yout + (int64_t)gx * a.ysx + (int64_t)c * a.ysc;
 #pragma unroll
-    for (int r = 0; r < TOY; ++r) {
-      const int gy = oy0 + r;
+    for (int r = 0; r < RG; ++r) {
+      const int gy = oy0 + rg * RG + r;
       if (gy < a.out_h) store2<TO, CHLAST>(pout + (int64_t)gy * a.ysy, a.ysc, ok2, o[r] * ps);
     }
   }
@@ -235,15 +246,33 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
 // ------------------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------------------
-constexpr int FLR_TOY = 16, FLR_TOX = 8;
+// tile variants (TOY, TOX, channels per workgroup, threads); IC2_FLR_VARIANT selects one (tuning)
+struct FlrVariant {
+  int toy, tox, cpb;
+};
+static const FlrVariant kFlrVariants[] = {{24, 8, 16}, {24, 8, 8}, {16, 8, 16}, {32, 8, 8}};
+static int flr_variant() {
+  static const int v = [] {
+    const char* e = getenv("IC2_FLR_VARIANT");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 0 && x < 4) ? x : 0;
+  }();
+  return v;
+}
 
 template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD>
 static int launch_delta(const FlrArgs& a, int delta, int grid, hipStream_t s) {
+  const int var = flr_variant();
+#define IC2_FLR_LAUNCH(DL, TY, TX, CPB, NT)                                                                      \
+  hipLaunchKernelGGL((flrelu_kernel<TI, TO, CHLAST, U, D, TU, TD, DL, TY, TX, CPB, NT>), dim3(grid), dim3(NT), 0, \
+                     s, a)
 #define IC2_FLR_CASE(DL)                                                                                         \
   case DL:                                                                                                       \
     if constexpr (DL < U) {                                                                                      \
-      hipLaunchKernelGGL((flrelu_kernel<TI, TO, CHLAST, U, D, TU, TD, DL, FLR_TOY, FLR_TOX>), dim3(grid),         \
-                         dim3(FLR_THREADS), 0, s, a);                                                            \
+      if (var == 0) IC2_FLR_LAUNCH(DL, 24, 8, 16, 256);                                                          \
+      else if (var == 1) IC2_FLR_LAUNCH(DL, 24, 8, 8, 128);                                                      \
+      else if (var == 2) IC2_FLR_LAUNCH(DL, 16, 8, 16, 128);                                                     \
+      else IC2_FLR_LAUNCH(DL, 32, 8, 8, 128);                                                                    \
       return IC2_OK;                                                                                             \
     }                                                                                                            \
     break;
@@ -254,6 +283,7 @@ static int launch_delta(const FlrArgs& a, int delta, int grid, hipStream_t s) {
     IC2_FLR_CASE(3)
   }
 #undef IC2_FLR_CASE
+#undef IC2_FLR_LAUNCH
   return IC2_E_UNSUPPORTED;
 }
 
@@ -283,6 +313,10 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
     set_error("%s: px0 and py0 differ mod up", name);
     return IC2_E_UNSUPPORTED;
   }
+  if (!(slope >= 0.f && slope <= 1.f && gain > 0.f)) {  // the fused activation uses max(v, slope*v)
+    set_error("%s: fused path needs 0 <= slope <= 1 and gain > 0", name);
+    return IC2_E_UNSUPPORTED;
+  }
   FlrArgs a;
   a.x = x; a.y = y; a.bias = b; a.post_scale = post_scale;
   if (chlast) {
@@ -296,15 +330,18 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   a.c_p = c_p;
   a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w;
   a.py0 = py0; a.px0 = px0;
-  a.tiles_x = (int)ceil_div(out_w, FLR_TOX);
-  a.tiles_y = (int)ceil_div(out_h, FLR_TOY);
-  a.cblocks = (int)ceil_div(a.c, FLR_CPB);
-  a.gain = gain; a.slope = slope; a.clamp = clamp;
+  const FlrVariant fv = kFlrVariants[flr_variant()];
+  a.tiles_x = (int)ceil_div(out_w, fv.tox);
+  a.tiles_y = (int)ceil_div(out_h, fv.toy);
+  a.cblocks = (int)ceil_div(a.c, fv.cpb);
+  a.slope = slope;
+  a.lim = clamp >= 0.f ? clamp / gain : INFINITY;
   for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
   for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;
   // NOTE: fu / fd are HOST pointers here (filters are layer constants; they travel in the kernarg)
   for (int t = 0; t < fu_taps; ++t) a.gu[t] = (fu ? (flip ? fu[t] : fu[fu_taps - 1 - t]) : 1.f) * (float)up;
   for (int t = 0; t < fd_taps; ++t) a.gd[t] = fd ? (flip ? fd[t] : fd[fd_taps - 1 - t]) : 1.f;
+  for (int t = 0; t < 12; ++t) a.gdg[t] = a.gd[t] * gain;
   const int64_t grid = (int64_t)n * a.tiles_y * a.tiles_x * a.cblocks;
   IC2_CHECK_ARG(grid < (1LL << 31), "%s: grid too large", name);
   hipStream_t s = as_stream(stream);
@@ -346,7 +383,7 @@ extern "C" int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_o
                                int fd_taps, const float* b, int up, int down, int px0, int px1, int py0, int py1,
                                float gain, float slope, float clamp, int flip, const float* post_scale,
                                void* stream) {
-  IC2_CHECK_ARG(c_p % FLR_CPB == 0, "flrelu_nhwc: c_p must be a multiple of %d", FLR_CPB);
+  IC2_CHECK_ARG(c_p % 16 == 0, "flrelu_nhwc: c_p must be a multiple of 16");
   return flrelu_common(x, y, dtype_in, dtype_out, true, n, c_p, c_p, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
                        fd_taps, b, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, post_scale, stream,
                        "flrelu_nhwc");

@@ -167,9 +167,29 @@ def test_filtered_lrelu_nchw(cuda, case, dtype):
 
 
 # ------------------------------------------------------------------ implicit-GEMM conv (MFMA)
-@pytest.mark.parametrize("cin,cout,size,pad", [(3, 32, 19, 1), (64, 96, 12, 1), (181, 128, 9, 2), (512, 512, 6, 2)])
+IGEMM_CASES = [(3, 32, 19, 1, 0), (64, 96, 12, 1, 0), (181, 128, 9, 2, 0), (512, 512, 6, 2, 0),
+               (256, 362, 10, 2, 1), (96, 64, 13, 1, 2), (128, 181, 11, 2, 3), (512, 256, 7, 2, 4),
+               (181, 192, 9, 2, 5)]
+
+
+@pytest.mark.parametrize("cin,cout,size,pad,tile", IGEMM_CASES)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_conv_igemm(cuda, cin, cout, size, pad, dtype):
+def test_conv_igemm(cuda, cin, cout, size, pad, tile, dtype, monkeypatch):
+    """Every bf16 tile instance (IC2_IGEMM_TILE forces it; read once per process, so the forced cases
+    run in a child process) against F.conv2d in fp64."""
+    if tile and dtype == torch.bfloat16:
+        import subprocess, sys
+        code = (f"import sys; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
+                f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad})")
+        env = dict(__import__('os').environ, IC2_IGEMM_TILE=str(tile))
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return
+    _conv_case(cin, cout, size, pad, dtype)
+
+
+def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16):
+    cuda = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(cin + cout)
     conv = torch.nn.Conv2d(cin, cout, 3, padding=pad)
     with torch.no_grad():

@@ -1,0 +1,87 @@
+"""Kernel microbenchmarks on the SG3-T-256 layer shapes (batch 32, bf16): FLR and implicit GEMM.
+
+    python tools/bench_kernels.py [flr|igemm] [variant-env-value ...]
+
+Each variant runs in a child process (the variant env var is read once per process).
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def child(kind):
+    import numpy as np
+    import torch
+    import image_compression_2_amd as ic2
+    from image_compression_2_amd import _native as nv
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=256, precision="bf16").to(dev)
+    res = {}
+    n = 32
+    for L in G.synthesis.layers()[:-1]:
+        s_in = int(L.in_size[0])
+        conv = s_in + 2
+        s_out = int(L.out_size[0])
+        if kind == "flr":
+            y = (torch.randn(n, conv, conv, L.cout_p, device=dev) * 2).to(torch.bfloat16)
+            out = torch.empty(n, s_out, s_out, L.cout_p, device=dev, dtype=torch.bfloat16)
+            def run():
+                nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.BF16, nv.BF16, n, L.cout_p, conv, conv, s_out,
+                        s_out, L._fu.ctypes.data_as(__import__("ctypes").c_void_p), L._fu.shape[0],
+                        L._fd.ctypes.data_as(__import__("ctypes").c_void_p), L._fd.shape[0], None, L.up_factor,
+                        L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0, None, nv.stream_of(y))
+            work = 0
+        else:
+            x = torch.randn(n, s_in, s_in, L.cin_p, device=dev).to(torch.bfloat16)
+            wp, _, bp = L.packed(torch.bfloat16)
+            out = torch.empty(n, conv, conv, L.cout_p, device=dev, dtype=torch.bfloat16)
+            def run():
+                nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(out), nv.BF16, nv.BF16, n, s_in, s_in,
+                        L.cin_p, L.cout_p, L.out_channels, 3, 3, 2, conv, conv, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0,
+                        1.0, nv.NHWC, nv.stream_of(x))
+            work = 2.0 * n * conv * conv * L.out_channels * 9 * L.in_channels
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 10
+        res[L.name] = (round(ms * 1e3, 1), round(work / (ms * 1e-3) / 1e12, 1) if work else None)
+    print(json.dumps(res))
+
+
+def main():
+    kind = sys.argv[1] if len(sys.argv) > 1 else "flr"
+    variants = sys.argv[2:] or ["0"]
+    env_name = "IC2_FLR_VARIANT" if kind == "flr" else "IC2_IGEMM_TILE"
+    table = {}
+    for v in variants:
+        env = dict(os.environ, **{env_name: v})
+        r = subprocess.run([sys.executable, __file__, "--child", kind], env=env, capture_output=True, text=True,
+                           timeout=600)
+        if r.returncode != 0:
+            print(f"variant {v} failed:\n{r.stderr[-2000:]}")
+            continue
+        table[v] = json.loads(r.stdout.strip().splitlines()[-1])
+    names = list(next(iter(table.values())).keys()) if table else []
+    print(f"{kind}: us (TFLOP/s) per layer, batch 32 bf16")
+    print(f"{'layer':14s}" + "".join(f"{'v' + v:>16s}" for v in table))
+    for nm in names:
+        print(f"{nm:14s}" + "".join(f"{str(table[v][nm]):>16s}" for v in table))
+    print(f"{'total us':14s}" + "".join(f"{sum(x[0] for x in table[v].values()):16.1f}" for v in table))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+    else:
+        main()
