@@ -3,7 +3,7 @@
 //   -> upfirdn2d(fd, down)]; called by SynthesisLayer.forward for every layer of
 // G.synthesis (/root/reference/stylegan3_hvae_full.py:274,329).
 //
-// One workgroup = one (sample, 16x8 output tile, 16-channel block).  Lanes own channel PAIRS
+// One workgroup = one (sample, 16x16 output tile (NHWC bf16; 24x8 otherwise), 16-channel block).  Lanes own channel PAIRS
 // (packed fp32 math, bf16x2 loads), the spatial FIR runs from registers with every tap index
 // resolved at compile time (polyphase: zero-inserted samples are never multiplied), and the
 // up-sampled grid lives only in LDS:
@@ -32,7 +32,7 @@ struct FlrArgs {
   int c, c_p;                   // valid channels, post_scale row stride
   int in_h, in_w, out_h, out_w;
   int py0, px0;                 // leading padding
-  int tiles_x, tiles_y, cblocks;
+  int tiles_x, tiles_y, cblocks, nimg;
   float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
   float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
   float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
@@ -114,10 +114,18 @@ __device__ __forceinline__ f2v act2(f2v v, float slope, float lim) {
 
 constexpr int FLR_S3 = 4;                // stage-3 row split (items = columns x pairs x FLR_S3)
 
+// First input sample j whose up-FIR tap t = U*j + DELTA - i lies in [0, TU): j = ceil((i - DELTA) / U),
+// clamped at 0.  The TU/U samples j, j+1, ... are exactly the polyphase taps of grid position i.
+template <int U, int DELTA>
+__host__ __device__ constexpr int up_first(int i) {
+  return i < DELTA ? 0 : (i - DELTA + U - 1) / U;
+}
+
 template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DELTA, int TOY, int TOX, int FLR_CPB,
           int FLR_THREADS>
-__global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
+__global__ void __launch_bounds__(FLR_THREADS) __attribute__((amdgpu_waves_per_eu(4))) flrelu_kernel(FlrArgs a) {
   constexpr int FLR_NCG = FLR_CPB / 2;  // channel pairs per workgroup
+  static_assert(TU % U == 0 && TD % D == 0, "polyphase loops assume whole phases");
   using G = FlrGeom<U, D, TU, TD, TOY, TOX>;
   using LT = typename std::conditional<std::is_same<TI, bf16_t>::value, uint32_t, f2v>::type;
   using LP = LdsPair<LT>;
@@ -168,9 +176,9 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     for (int i = 0; i < RAY; ++i) {
       f2v acc = f2v{0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < NINY; ++j) {
-        const int t = U * j + DELTA - i;
-        if (t >= 0 && t < TU) acc += a.gu[t] * in[j];
+      for (int m = 0; m < TU / U; ++m) {  // the TU/U polyphase taps landing on grid row i
+        const int j = up_first<U, DELTA>(i) + m;
+        if (j < NINY) acc += a.gu[U * j + DELTA - i] * in[j];
       }
       buf[(i * NINXP + xs) * NCG + cg] = LP::pack(acc);
     }
@@ -191,15 +199,15 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     for (int k = 0; k < RAX; ++k) {
       f2v v = f2v{0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < NINX; ++j) {
-        const int t = U * j + DELTA - k;
-        if (t >= 0 && t < TU) v += a.gu[t] * in[j];
+      for (int m = 0; m < TU / U; ++m) {
+        const int j = up_first<U, DELTA>(k) + m;
+        if (j < NINX) v += a.gu[U * j + DELTA - k] * in[j];
       }
       v = act2(v, a.slope, a.lim);
 #pragma unroll
-      for (int o = 0; o < TOX; ++o) {
-        const int t = k - o * D;
-        if (t >= 0 && t < TD) d[o] += a.gdg[t] * v;
+      for (int m = 0; m < TD / D; ++m) {  // outputs o with 0 <= k - o*D < TD
+        const int o = k / D - m;
+        if (o >= 0 && o < TOX) d[o] += a.gdg[k - o * D] * v;
       }
     }
 #pragma unroll
@@ -227,9 +235,9 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
     for (int ii = 0; ii < RGI; ++ii) {
       const f2v v = LP::unpack(buf[((i0 + ii) * NINXP + ox) * NCG + cg]);
 #pragma unroll
-      for (int r = 0; r < RG; ++r) {
-        const int t = ii - r * D;
-        if (t >= 0 && t < TD) o[r] += a.gd[t] * v;
+      for (int m = 0; m < TD / D; ++m) {
+        const int r = ii / D - m;
+        if (r >= 0 && r < RG) o[r] += a.gd[ii - r * D] * v;
       }
     }
     f2v ps = f2v{1.f, 1.f};
@@ -246,51 +254,69 @@ __global__ void __launch_bounds__(FLR_THREADS) flrelu_kernel(FlrArgs a) {
 // ------------------------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------------------------
-// tile variants (TOY, TOX, channels per workgroup, threads); IC2_FLR_VARIANT selects one (tuning)
-struct FlrVariant {
-  int toy, tox, cpb;
+// Tile geometries (TOY, TOX, channels per workgroup, threads).  The bf16 NHWC instances (the synthesis
+// throughput path) are tuned per up-factor; every other dtype/layout uses geometry 0 only.
+// IC2_FLR_VARIANT=k forces geometry k on the bf16 NHWC path (tuning, tools/bench_kernels.py).
+struct FlrGeomSel {
+  int toy, tox, cpb, nt;
 };
-static const FlrVariant kFlrVariants[] = {{24, 8, 16}, {24, 8, 8}, {16, 8, 16}, {32, 8, 8}};
+static const FlrGeomSel kFlrGeoms[] = {
+    {24, 8, 16, 256}, {16, 8, 16, 256}, {16, 16, 16, 256}, {8, 16, 16, 256}, {12, 16, 16, 256}, {16, 16, 8, 128}};
+constexpr int kNumFlrGeoms = sizeof(kFlrGeoms) / sizeof(kFlrGeoms[0]);
 static int flr_variant() {
   static const int v = [] {
     const char* e = getenv("IC2_FLR_VARIANT");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 0 && x < 4) ? x : 0;
+    const int x = e ? atoi(e) : -1;
+    return (x >= 0 && x < kNumFlrGeoms) ? x : -1;
   }();
   return v;
 }
+static int flr_pick(bool tuned, int up) {
+  if (!tuned) return 0;
+  if (flr_variant() >= 0) return flr_variant();
+  (void)up;
+  return 2;  // 16x16 tiles: fastest on every SG3-T-256 layer but the 36^2 ones (profiles/r1_flr_variants.txt)
+}
+
+template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD, int DL>
+static int launch_geom(const FlrArgs& a, int geom, int grid, hipStream_t s) {
+#define IC2_FLR_LAUNCH(TY, TX, CPB, NT)                                                                            \
+  hipLaunchKernelGGL((flrelu_kernel<TI, TO, CHLAST, U, D, TU, TD, DL, TY, TX, CPB, NT>), dim3(grid), dim3(NT), 0, s, a)
+  constexpr bool tuned = CHLAST && std::is_same<TI, bf16_t>::value;
+  if constexpr (tuned) {
+    switch (geom) {
+      case 1: IC2_FLR_LAUNCH(16, 8, 16, 256); return IC2_OK;
+      case 2: IC2_FLR_LAUNCH(16, 16, 16, 256); return IC2_OK;
+      case 3: IC2_FLR_LAUNCH(8, 16, 16, 256); return IC2_OK;
+      case 4: IC2_FLR_LAUNCH(12, 16, 16, 256); return IC2_OK;
+      case 5: IC2_FLR_LAUNCH(16, 16, 8, 128); return IC2_OK;
+      default: break;
+    }
+  }
+  if (geom != 0) return IC2_E_UNSUPPORTED;
+  IC2_FLR_LAUNCH(24, 8, 16, 256);
+  return IC2_OK;
+#undef IC2_FLR_LAUNCH
+}
 
 template <typename TI, typename TO, bool CHLAST, int U, int D, int TU, int TD>
-static int launch_delta(const FlrArgs& a, int delta, int grid, hipStream_t s) {
-  const int var = flr_variant();
-#define IC2_FLR_LAUNCH(DL, TY, TX, CPB, NT)                                                                      \
-  hipLaunchKernelGGL((flrelu_kernel<TI, TO, CHLAST, U, D, TU, TD, DL, TY, TX, CPB, NT>), dim3(grid), dim3(NT), 0, \
-                     s, a)
-#define IC2_FLR_CASE(DL)                                                                                         \
-  case DL:                                                                                                       \
-    if constexpr (DL < U) {                                                                                      \
-      if (var == 0) IC2_FLR_LAUNCH(DL, 24, 8, 16, 256);                                                          \
-      else if (var == 1) IC2_FLR_LAUNCH(DL, 24, 8, 8, 128);                                                      \
-      else if (var == 2) IC2_FLR_LAUNCH(DL, 16, 8, 16, 128);                                                     \
-      else IC2_FLR_LAUNCH(DL, 32, 8, 8, 128);                                                                    \
-      return IC2_OK;                                                                                             \
-    }                                                                                                            \
-    break;
+static int launch_delta(const FlrArgs& a, int delta, int geom, int grid, hipStream_t s) {
   switch (delta) {
-    IC2_FLR_CASE(0)
-    IC2_FLR_CASE(1)
-    IC2_FLR_CASE(2)
-    IC2_FLR_CASE(3)
+    case 0: return launch_geom<TI, TO, CHLAST, U, D, TU, TD, 0>(a, geom, grid, s);
+    case 1: return launch_geom<TI, TO, CHLAST, U, D, TU, TD, 1>(a, geom, grid, s);
+    case 2: if constexpr (U > 2) return launch_geom<TI, TO, CHLAST, U, D, TU, TD, 2>(a, geom, grid, s); break;
+    case 3: if constexpr (U > 3) return launch_geom<TI, TO, CHLAST, U, D, TU, TD, 3>(a, geom, grid, s); break;
   }
-#undef IC2_FLR_CASE
-#undef IC2_FLR_LAUNCH
   return IC2_E_UNSUPPORTED;
 }
 
 template <typename TI, typename TO, bool CHLAST>
-static int launch_cfg(const FlrArgs& a, int up, int down, int tu, int td, int delta, int grid, hipStream_t s) {
-  if (up == 2 && down == 2 && tu == 12 && td == 12) return launch_delta<TI, TO, CHLAST, 2, 2, 12, 12>(a, delta, grid, s);
-  if (up == 4 && down == 2 && tu == 24 && td == 12) return launch_delta<TI, TO, CHLAST, 4, 2, 24, 12>(a, delta, grid, s);
+static int launch_cfg(const FlrArgs& a, int up, int down, int tu, int td, int delta, int geom, int grid,
+                      hipStream_t s) {
+  if (up == 2 && down == 2 && tu == 12 && td == 12)
+    return launch_delta<TI, TO, CHLAST, 2, 2, 12, 12>(a, delta, geom, grid, s);
+  if (up == 4 && down == 2 && tu == 24 && td == 12)
+    return launch_delta<TI, TO, CHLAST, 4, 2, 24, 12>(a, delta, geom, grid, s);
   return IC2_E_UNSUPPORTED;
 }
 
@@ -330,10 +356,12 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   a.c_p = c_p;
   a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w;
   a.py0 = py0; a.px0 = px0;
-  const FlrVariant fv = kFlrVariants[flr_variant()];
+  const int geom = flr_pick(chlast && dtype_in == IC2_BF16 && dtype_out == IC2_BF16, up);
+  const FlrGeomSel fv = kFlrGeoms[geom];
   a.tiles_x = (int)ceil_div(out_w, fv.tox);
   a.tiles_y = (int)ceil_div(out_h, fv.toy);
   a.cblocks = (int)ceil_div(a.c, fv.cpb);
+  a.nimg = n;
   a.slope = slope;
   a.lim = clamp >= 0.f ? clamp / gain : INFINITY;
   for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
@@ -347,11 +375,11 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   hipStream_t s = as_stream(stream);
   int rc;
   if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16)
-    rc = chlast ? launch_cfg<bf16_t, bf16_t, true>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s)
-                : launch_cfg<bf16_t, bf16_t, false>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s);
+    rc = chlast ? launch_cfg<bf16_t, bf16_t, true>(a, up, down, fu_taps, fd_taps, dx, geom, (int)grid, s)
+                : launch_cfg<bf16_t, bf16_t, false>(a, up, down, fu_taps, fd_taps, dx, geom, (int)grid, s);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_F32)
-    rc = chlast ? launch_cfg<float, float, true>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s)
-                : launch_cfg<float, float, false>(a, up, down, fu_taps, fd_taps, dx, (int)grid, s);
+    rc = chlast ? launch_cfg<float, float, true>(a, up, down, fu_taps, fd_taps, dx, geom, (int)grid, s)
+                : launch_cfg<float, float, false>(a, up, down, fu_taps, fd_taps, dx, geom, (int)grid, s);
   else {
     set_error("%s: unsupported dtype pair %d -> %d", name, dtype_in, dtype_out);
     return IC2_E_INVALID;

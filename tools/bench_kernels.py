@@ -23,7 +23,8 @@ def child(kind):
     G = ic2.Generator(img_resolution=256, precision="bf16").to(dev)
     res = {}
     n = 32
-    for L in G.synthesis.layers()[:-1]:
+    for name in G.synthesis.layer_names[:-1]:
+        L = getattr(G.synthesis, name)
         s_in = int(L.in_size[0])
         conv = s_in + 2
         s_out = int(L.out_size[0])
@@ -55,7 +56,7 @@ def child(kind):
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / 10
-        res[L.name] = (round(ms * 1e3, 1), round(work / (ms * 1e-3) / 1e12, 1) if work else None)
+        res[name] = (round(ms * 1e3, 1), round(work / (ms * 1e-3) / 1e12, 1) if work else None)
     print(json.dumps(res))
 
 
@@ -65,7 +66,11 @@ def main():
     env_name = "IC2_FLR_VARIANT" if kind == "flr" else "IC2_IGEMM_TILE"
     table = {}
     for v in variants:
-        env = dict(os.environ, **{env_name: v})
+        # "v" or "v,p" (p = IC2_FLR_PERSIST for flr, IC2_IGEMM_SPLITK for igemm)
+        parts = v.split(",")
+        env = dict(os.environ, **{env_name: parts[0]})
+        if len(parts) > 1:
+            env["IC2_FLR_PERSIST" if kind == "flr" else "IC2_IGEMM_SPLITK"] = parts[1]
         r = subprocess.run([sys.executable, __file__, "--child", kind], env=env, capture_output=True, text=True,
                            timeout=600)
         if r.returncode != 0:
