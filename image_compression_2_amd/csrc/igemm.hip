@@ -38,7 +38,8 @@ struct IgemmArgs {
   int K;        // kh * kw * cin_p
   int nq;       // K / 32
   int tiles_o;  // ceil(cout_p / BO)
-  int nblocks;
+  int nblocks;  // tiles_o * tiles_p
+  int group;    // p-tiles per o-sweep (tile_coords)
   int act;
   float slope, act_gain, clamp, out_mul;
   int out_layout, out_dtype;
@@ -61,179 +62,22 @@ struct IgCfg {
   __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
 };
 
-template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
-__global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
-  using C = IgCfg<BF16, BO, BP, WGO, WGP, NSTAGE>;
-  constexpr int EPC = C::EPC, ESZ = C::ESZ, I = C::I, J = C::J, NIW = C::NIW, NIX = C::NIX;
-  static_assert(C::I >= 1 && C::J >= 1, "wave tile smaller than one MFMA tile");
-  static_assert(C::NIW_T >= 1 && C::NIX_T >= 1, "tile smaller than one DMA instruction");
-  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * C::STAGEB];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int wo_ = wid / WGP, wp_ = wid % WGP;
-
-  // XCD-aware, bijective block remap: blocks b and b+8 share an XCD -> give each XCD a contiguous
-  // run of logical tiles (tiles adjacent in p share input rows; same-p tiles share the X panel).
-  int logical;
-  {
-    const int b = blockIdx.x;
-    const int xcd = b & 7, loc = b >> 3;
-    const int q8 = a.nblocks >> 3, r8 = a.nblocks & 7;
-    logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  }
-  const int o_tile = logical % a.tiles_o;
-  const int p_tile = logical / a.tiles_o;
-  const int o0 = o_tile * BO;
-  const int m0 = p_tile * BP;
-
-  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
-  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
-
-  // ---- per-lane DMA slots.  Instruction g of an operand fills LDS bytes [g KiB, g+1 KiB): lane l
-  // lands on row g*(1024/ROWB) + l/(ROWB/16), physical slot l%(ROWB/16) = logical chunk slot^swz(row).
-  // Waves beyond an operand's instruction count repeat its last instruction (identical bytes).
-  int x_nb[NIX], x_oy[NIX], x_ox[NIX], x_ch[NIX], x_seg[NIX];
-  bool x_ok[NIX];
-  int64_t w_off[NIW];
-  bool w_ok[NIW];
-  int w_seg[NIW];
+// Epilogue shared by both kernels: lane holds C[o = obase + 16i + 4*fh + r][p = pbase + 16j + fr].
+// y = act(acc * oscale[n][o] + bias[o]) * out_mul, stored NHWC (bf16/f32) or NCHW (f32, o < cout_valid).
+template <int I, int J>
+__device__ __forceinline__ void ig_epilogue(const IgemmArgs& a, const f32x4 (&acc)[I][J], int obase, int pbase, int fr,
+                                            int fh) {
   const int hw = a.ho * a.wo;
-#pragma unroll
-  for (int k = 0; k < NIX; ++k) {
-    const int g = min(wid_u + C::NW * k, C::NIX_T - 1);
-    x_seg[k] = g * 1024;
-    const int off = g * 1024 + lane * 16;
-    const int row = off / C::ROWB;
-    x_ch[k] = ((off % C::ROWB) >> 4) ^ C::swz(row);
-    const int m = m0 + row;
-    x_ok[k] = m < a.M;
-    const int mm = x_ok[k] ? m : 0;
-    const int nn = mm / hw;
-    const int rem = mm - nn * hw;
-    const int oy = rem / a.wo;
-    x_nb[k] = nn * a.h;
-    x_oy[k] = oy - a.pad;
-    x_ox[k] = rem - oy * a.wo - a.pad;
-  }
-#pragma unroll
-  for (int k = 0; k < NIW; ++k) {
-    const int g = min(wid_u + C::NW * k, C::NIW_T - 1);
-    w_seg[k] = g * 1024;
-    const int off = g * 1024 + lane * 16;
-    const int row = off / C::ROWB;
-    const int chl = ((off % C::ROWB) >> 4) ^ C::swz(row);
-    const int o = o0 + row;
-    w_ok[k] = o < a.cout_p;
-    w_off[k] = (int64_t)(w_ok[k] ? o : 0) * a.K * ESZ + chl * 16;
-  }
-  const int CB = a.cin_p >> 5;
-
-#define IC2_IG_ISSUE(q_, buf_)                                                                                \
-  {                                                                                                          \
-    const int q__ = (q_);                                                                                    \
-    const int tap = q__ / CB;                                                                                \
-    const int cbk = q__ - tap * CB;                                                                          \
-    const int ky = tap / a.kw;                                                                               \
-    const int kx = tap - ky * a.kw;                                                                          \
-    char* wl_ = lds + (buf_) * C::STAGEB;                                                                    \
-    char* xl_ = wl_ + C::WB;                                                                                 \
-    _Pragma("unroll") for (int k = 0; k < NIW; ++k) {                                                        \
-      const void* ws = w_ok[k] ? (const void*)(wg + w_off[k] + (int64_t)q__ * 32 * ESZ) : zero_line();       \
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ws,                     \
-                                       (__attribute__((address_space(3))) void*)(wl_ + w_seg[k]), 16, 0, 0); \
-    }                                                                                                        \
-    _Pragma("unroll") for (int k = 0; k < NIX; ++k) {                                                        \
-      const int iy = x_oy[k] + ky;                                                                           \
-      const int ix = x_ox[k] + kx;                                                                           \
-      const bool ok = x_ok[k] && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;              \
-      const int64_t e = ((int64_t)(x_nb[k] + iy) * a.w_ + ix) * a.cin_p + cbk * 32 + x_ch[k] * EPC;          \
-      const void* xs = ok ? (const void*)(xg + e * ESZ) : zero_line();                                       \
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)xs,                     \
-                                       (__attribute__((address_space(3))) void*)(xl_ + x_seg[k]), 16, 0, 0); \
-    }                                                                                                        \
-  }
-
-  f32x4 acc[I][J];
-#pragma unroll
-  for (int i = 0; i < I; ++i)
-#pragma unroll
-    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int s_ = 0; s_ < NSTAGE - 1; ++s_) IC2_IG_ISSUE(s_ < a.nq ? s_ : a.nq - 1, s_);
-
-  const int fr = lane & 15;
-  const int fh = lane >> 4;
-
-  for (int q = 0; q < a.nq; ++q) {
-    const int cur = q % NSTAGE;
-    if constexpr (NSTAGE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * C::PER) : "memory");
-    __builtin_amdgcn_s_barrier();  // chunk q landed for every wave; chunk q-1 fully read
-    __builtin_amdgcn_sched_barrier(0);
-    {
-      const int qn = q + NSTAGE - 1;
-      IC2_IG_ISSUE(qn < a.nq ? qn : a.nq - 1, qn % NSTAGE);  // refill the slot chunk q-1 used
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const char* wl = lds + cur * C::STAGEB;
-    const char* xl = wl + C::WB;
-    if constexpr (BF16) {
-      bf16x8 bfr[J];
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int row = wp_ * C::TP + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(xl + C::off(row, fh));
-      }
-#pragma unroll
-      for (int i = 0; i < I; ++i) {
-        const int row = wo_ * C::TO + i * 16 + fr;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + C::off(row, fh));
-#pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-      }
-    } else {
-      // lane group fh uses k = 8*fh + s for step s: chunks 2fh (s<4) and 2fh+1 (s>=4)
-      f32x4 af[I][2], bfr[J][2];
-#pragma unroll
-      for (int i = 0; i < I; ++i) {
-        const int row = wo_ * C::TO + i * 16 + fr;
-        af[i][0] = *reinterpret_cast<const f32x4*>(wl + C::off(row, 2 * fh));
-        af[i][1] = *reinterpret_cast<const f32x4*>(wl + C::off(row, 2 * fh + 1));
-      }
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int row = wp_ * C::TP + j * 16 + fr;
-        bfr[j][0] = *reinterpret_cast<const f32x4*>(xl + C::off(row, 2 * fh));
-        bfr[j][1] = *reinterpret_cast<const f32x4*>(xl + C::off(row, 2 * fh + 1));
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-#pragma unroll
-        for (int i = 0; i < I; ++i)
-#pragma unroll
-          for (int j = 0; j < J; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s >> 2][s & 3], bfr[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // every MFMA of this chunk before the next wait
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the redundant tail DMAs before exit
-#undef IC2_IG_ISSUE
-
-  // ---- epilogue: lane holds C[o = base + 4*fh + r][p = base + fr]
   const bool has_os = a.oscale != nullptr, has_b = a.bias != nullptr;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int p = m0 + wp_ * C::TP + j * 16 + fr;
+    const int p = pbase + j * 16 + fr;
     if (p >= a.M) continue;
     const int nn = p / hw;
     const int pix = p - nn * hw;
 #pragma unroll
     for (int i = 0; i < I; ++i) {
-      const int ob = o0 + wo_ * C::TO + i * 16 + 4 * fh;
+      const int ob = obase + i * 16 + 4 * fh;
       if (ob >= a.cout_p) continue;
       float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), bi = make_float4(0.f, 0.f, 0.f, 0.f);
       if (has_os) sc = *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob);
@@ -264,6 +108,410 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
       }
     }
   }
+}
+
+// XCD-aware, bijective block remap: blocks b and b+8 share an XCD -> give each XCD a contiguous run
+// of logical tiles (tiles adjacent in p share input rows; same-p tiles share the X panel).
+__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
+  const int xcd = b & 7, loc = b >> 3;
+  const int q8 = nblocks >> 3, r8 = nblocks & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+}
+
+// logical tile -> (o_tile, p_tile), bijective: runs of `group` consecutive p-tiles sweep one o-tile at a
+// time, so the blocks resident on one XCD at once share a single weight panel in its L2 (all o-tiles of
+// a p-tile side by side would keep tiles_o panels live).  The last run may be shorter.
+__device__ __forceinline__ void tile_coords(int logical, int tiles_o, int tiles_p, int group, int& o_tile,
+                                            int& p_tile) {
+  const int per = group * tiles_o;
+  const int gi = logical / per;
+  const int rem = logical - gi * per;
+  const int gsz = min(group, tiles_p - gi * group);
+  o_tile = rem / gsz;
+  p_tile = gi * group + (rem - o_tile * gsz);
+}
+
+template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
+__global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
+  using C = IgCfg<BF16, BO, BP, WGO, WGP, NSTAGE>;
+  constexpr int EPC = C::EPC, ESZ = C::ESZ, I = C::I, J = C::J, NIW = C::NIW, NIX = C::NIX;
+  static_assert(C::I >= 1 && C::J >= 1, "wave tile smaller than one MFMA tile");
+  static_assert(C::NIW_T >= 1 && C::NIX_T >= 1, "tile smaller than one DMA instruction");
+  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * C::STAGEB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const int wo_ = wid / WGP, wp_ = wid % WGP;
+
+  const int logical = xcd_remap(blockIdx.x, a.nblocks);
+  int o_tile, p_tile;
+  tile_coords(logical, a.tiles_o, a.nblocks / a.tiles_o, a.group, o_tile, p_tile);
+  const int o0 = o_tile * BO;
+  const int m0 = p_tile * BP;
+
+  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
+  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
+
+  // ---- per-lane DMA slots.  Instruction g of an operand fills LDS bytes [g KiB, g+1 KiB): lane l
+  // lands on row g*(1024/ROWB) + l/(ROWB/16), physical slot l%(ROWB/16) = logical chunk slot^swz(row).
+  // Waves beyond an operand's instruction count repeat its last instruction (identical bytes).
+  // X: per-lane base pointer at tap (0,0) of the lane's pixel; a chunk adds a uniform byte offset.
+  const char* x_base[NIX];
+  int x_oy[NIX], x_ox[NIX], x_seg[NIX];
+  const char* w_base[NIW];
+  int w_seg[NIW];
+  const int hw = a.ho * a.wo;
+#pragma unroll
+  for (int k = 0; k < NIX; ++k) {
+    const int g = min(wid_u + C::NW * k, C::NIX_T - 1);
+    x_seg[k] = g * 1024;
+    const int off = g * 1024 + lane * 16;
+    const int row = off / C::ROWB;
+    const int ch = ((off % C::ROWB) >> 4) ^ C::swz(row);
+    const int m = m0 + row;
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int nn = mm / hw;
+    const int rem = mm - nn * hw;
+    const int oy = rem / a.wo;
+    const int ox = rem - oy * a.wo;
+    // rows past M get an out-of-range y so every tap reads the zero line
+    x_oy[k] = ok ? oy - a.pad : -(1 << 20);
+    x_ox[k] = ox - a.pad;
+    const int64_t e = ((int64_t)(nn * a.h + x_oy[k]) * a.w_ + x_ox[k]) * a.cin_p + ch * EPC;
+    x_base[k] = xg + (ok ? e : 0) * ESZ;
+  }
+#pragma unroll
+  for (int k = 0; k < NIW; ++k) {
+    const int g = min(wid_u + C::NW * k, C::NIW_T - 1);
+    w_seg[k] = g * 1024;
+    const int off = g * 1024 + lane * 16;
+    const int row = off / C::ROWB;
+    const int chl = ((off % C::ROWB) >> 4) ^ C::swz(row);
+    const int o = o0 + row;
+    w_base[k] = o < a.cout_p ? wg + (int64_t)o * a.K * ESZ + chl * 16 : nullptr;
+  }
+  const int CB = a.cin_p >> 5;
+  // chunk cursor of the next DMA (uniform): chunk index, its tap (ky, kx) and 32-channel block
+  int iq = 0, icb = 0, ikx = 0, iky = 0;
+  const int64_t xrow = (int64_t)a.w_ * a.cin_p * ESZ;
+
+#define IC2_IG_ISSUE(buf_)                                                                                    \
+  {                                                                                                          \
+    char* wl_ = lds + (buf_) * C::STAGEB;                                                                    \
+    char* xl_ = wl_ + C::WB;                                                                                 \
+    const int64_t wq = (int64_t)iq * 32 * ESZ;                                                               \
+    const int64_t xq = iky * xrow + ((int64_t)ikx * a.cin_p + icb * 32) * ESZ;                               \
+    _Pragma("unroll") for (int k = 0; k < NIW; ++k) {                                                        \
+      const void* ws = w_base[k] ? (const void*)(w_base[k] + wq) : zero_line();                              \
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ws,                     \
+                                       (__attribute__((address_space(3))) void*)(wl_ + w_seg[k]), 16, 0, 0); \
+    }                                                                                                        \
+    _Pragma("unroll") for (int k = 0; k < NIX; ++k) {                                                        \
+      const bool ok = (unsigned)(x_oy[k] + iky) < (unsigned)a.h && (unsigned)(x_ox[k] + ikx) < (unsigned)a.w_; \
+      const void* xs = ok ? (const void*)(x_base[k] + xq) : zero_line();                                     \
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)xs,                     \
+                                       (__attribute__((address_space(3))) void*)(xl_ + x_seg[k]), 16, 0, 0); \
+    }                                                                                                        \
+    { /* advance (branch-free); past the end the last chunk is re-issued (never consumed) */               \
+      const int adv = iq + 1 < a.nq;                                                                         \
+      iq += adv;                                                                                             \
+      icb += adv;                                                                                            \
+      const int wrap = icb == CB;                                                                            \
+      icb = wrap ? 0 : icb;                                                                                  \
+      ikx += wrap;                                                                                           \
+      const int wrap2 = ikx == a.kw;                                                                         \
+      ikx = wrap2 ? 0 : ikx;                                                                                 \
+      iky += wrap2;                                                                                          \
+    }                                                                                                        \
+  }
+
+  f32x4 acc[I][J];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s_ = 0; s_ < NSTAGE - 1; ++s_) IC2_IG_ISSUE(s_);
+
+  const int fr = lane & 15;
+  const int fh = lane >> 4;
+
+  for (int q = 0; q < a.nq; ++q) {
+    const int cur = q % NSTAGE;
+    if constexpr (NSTAGE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * C::PER) : "memory");
+    __builtin_amdgcn_s_barrier();  // chunk q landed for every wave; chunk q-1 fully read
+    __builtin_amdgcn_sched_barrier(0);
+    const char* wl = lds + cur * C::STAGEB;
+    const char* xl = wl + C::WB;
+    if constexpr (BF16) {
+      // all fragment reads first (B, then A in use order), then the refill of the slot chunk q-1 used
+      // (its address math runs under the read latency), then the MFMAs: group i waits only for its
+      // own A fragment (counted lgkmcnt), the later reads stay in flight
+      bf16x8 bfr[J], af[I];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int row = wp_ * C::TP + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(xl + C::off(row, fh));
+      }
+#pragma unroll
+      for (int i = 0; i < I; ++i) af[i] = *reinterpret_cast<const bf16x8*>(wl + C::off(wo_ * C::TO + i * 16 + fr, fh));
+      __builtin_amdgcn_sched_barrier(0);
+      IC2_IG_ISSUE((q + NSTAGE - 1) % NSTAGE);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      IC2_IG_ISSUE((q + NSTAGE - 1) % NSTAGE);
+      __builtin_amdgcn_sched_barrier(0);
+      // lane group fh uses k = 8*fh + s for step s: chunks 2fh (s<4) and 2fh+1 (s>=4)
+      f32x4 af[I][2], bfr[J][2];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int row = wo_ * C::TO + i * 16 + fr;
+        af[i][0] = *reinterpret_cast<const f32x4*>(wl + C::off(row, 2 * fh));
+        af[i][1] = *reinterpret_cast<const f32x4*>(wl + C::off(row, 2 * fh + 1));
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int row = wp_ * C::TP + j * 16 + fr;
+        bfr[j][0] = *reinterpret_cast<const f32x4*>(xl + C::off(row, 2 * fh));
+        bfr[j][1] = *reinterpret_cast<const f32x4*>(xl + C::off(row, 2 * fh + 1));
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < I; ++i)
+#pragma unroll
+          for (int j = 0; j < J; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s >> 2][s & 3], bfr[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every MFMA of this chunk before the next wait
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the redundant tail DMAs before exit
+#undef IC2_IG_ISSUE
+
+  ig_epilogue<I, J>(a, acc, o0 + wo_ * C::TO, m0 + wp_ * C::TP, fr, fh);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 256 x 256 bf16 tile, 64-deep K-tiles (64 channels of one tap), 8 waves = 2 o-groups x 4 p-groups,
+// each wave owning 128 x 64 outputs.  Eight phases per iteration (two K-tiles, LDS double buffer):
+// phase = (ds_read the quadrant's fragments, DMA one half-tile, [counted vmcnt], s_barrier,
+// 16 MFMAs at raised priority, s_barrier).  The o-group 1 waves run one barrier behind group 0, so on
+// every SIMD (one wave of each group) one wave's MFMAs overlap the other's LDS reads and DMA issue.
+//   quadrant per phase&3 : (qm,qn) = (0,0) (0,1) (1,1) (1,0); reads A(qm)+B(qn), B(1), A(1), B(0)
+//   half-tile restaged   : ph0 buf1.A1<-t+1  ph1 buf1.B0<-t+1  ph2..5 buf0.{A0,B1,A1,B0}<-t+2
+//                          ph6 buf1.A0<-t+3  ph7 buf1.B1<-t+3      (t = 2*iteration)
+// Every half is restaged >= 2 phases after its last read (WAR) and read >= 1 phase after the
+// vmcnt(4) + barrier that retires it (RAW: waits in phases 3 and 7).  Half-tile qm of A = the rows
+// {128*g + 64*qm + [0, 64)}; half-tile qn of B = the rows {64*g + 32*qn + [0, 32)}: 16 KiB, two
+// 1-KiB DMA instructions per wave.  LDS rows are 128 B, 16-B chunk c stored at c ^ ((row >> 1) & 7)
+// (conflict-free ds_read_b128 for the fragment lane groups).
+constexpr int G8_BUF = 65536, G8_BOFF = 32768;  // bytes: one K-tile buffer, B offset in it
+constexpr uint32_t kOob = 0x7ffffff0u;            // num_records of a live descriptor = the zero-answer offset
+constexpr int kRsrcWord3 = 0x00020000;            // raw buffer descriptor word 3 (gfx9 family)
+__device__ __forceinline__ int g8_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int g8_arow(int qm, int g, int l) { return (g >> 3) * 128 + qm * 64 + (g & 7) * 8 + l; }
+__device__ __forceinline__ int g8_brow(int qn, int g, int l) { return (g >> 2) * 64 + qn * 32 + (g & 3) * 8 + l; }
+
+__global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * G8_BUF];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid_u >> 2;  // o-group (= ping-pong group)
+  const int wp_ = wid_u & 3;
+  const int logical = xcd_remap(blockIdx.x, a.nblocks);
+  int o_tile, p_tile;
+  tile_coords(logical, a.tiles_o, a.nblocks / a.tiles_o, a.group, o_tile, p_tile);
+  const int o0 = o_tile * 256;
+  const int m0 = p_tile * 256;
+  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
+  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
+
+  // per-lane DMA sources: [half][instruction]; instruction k of wave w moves row block g = w + 8k.
+  // Buffer loads (raw, stride 0): the per-K-tile part of the address is a scalar descriptor base, the
+  // per-lane part a constant 32-bit offset; a tap outside the image / a row past M or cout_p gets the
+  // offset kOob (>= num_records), which the hardware answers with zeros.  No per-lane 64-bit math.
+  uint32_t w_off[2][2], x_off[2][2], x_tap[2][2];
+  const int hw = a.ho * a.wo;
+  const int lrow = lane >> 3;                    // row within the 8-row block
+  const int pch = lane & 7;                      // physical 16-B chunk written by this lane
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int g = wid_u + 8 * k;
+      const int ar = g8_arow(h, g, lrow);
+      const int o = o0 + ar;
+      w_off[h][k] = o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((ar >> 1) & 7)) << 4)) : kOob;
+      const int br = g8_brow(h, g, lrow);
+      const int m = m0 + br;
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      const int nn = mm / hw;
+      const int rem = mm - nn * hw;
+      const int oy = rem / a.wo;
+      const int ox = rem - oy * a.wo;
+      // offset of the output pixel's own (oy, ox) position; the descriptor base carries the tap shift
+      x_off[h][k] = (uint32_t)((((nn * a.h + oy) * a.w_ + ox) * a.cin_p + ((pch ^ ((br >> 1) & 7)) << 3)) * 2);
+      uint32_t mask = 0;
+      for (int ky = 0; ky < a.kh; ++ky)
+        for (int kx = 0; kx < a.kw; ++kx) {
+          const bool in = ok && (unsigned)(oy - a.pad + ky) < (unsigned)a.h && (unsigned)(ox - a.pad + kx) < (unsigned)a.w_;
+          mask |= (uint32_t)in << (ky * a.kw + kx);
+        }
+      x_tap[h][k] = mask;
+    }
+  const int CB = a.cin_p >> 6;
+
+  // K-tile cursor (uniform): tile index, tap (ky, kx), 64-channel block
+  struct Cur {
+    int t, ky, kx, cb;
+  };
+  auto advance = [&](Cur c) {
+    c.t += 1;
+    c.cb += 1;
+    const int wrap = c.cb == CB;
+    c.cb = wrap ? 0 : c.cb;
+    c.kx += wrap;
+    const int wrap2 = c.kx == a.kw;
+    c.kx = wrap2 ? 0 : c.kx;
+    c.ky += wrap2;
+    return c;
+  };
+
+#define IC2_G8_ISSUE_A(h_, buf_, c_)                                                                          \
+  {                                                                                                          \
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(                                     \
+        (void*)(wg + (int64_t)(c_).t * 128), 0, (c_).t < a.nq ? kOob : 0, kRsrcWord3);                        \
+    _Pragma("unroll") for (int k = 0; k < 2; ++k)                                                            \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G8_BUF + \
+                                                                                       g8_arow(h_, wid_u + 8 * k, 0) * 128), \
+                                               16, w_off[h_][k], 0, 0, 0);                                   \
+  }
+#define IC2_G8_ISSUE_B(h_, buf_, c_)                                                                          \
+  {                                                                                                          \
+    const int tap = (c_).ky * a.kw + (c_).kx;                                                                \
+    const int64_t sh = ((int64_t)((c_).ky - a.pad) * a.w_ + ((c_).kx - a.pad)) * a.cin_p * 2 + (c_).cb * 128;  \
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(xg + sh), 0,                  \
+                                                                        (c_).t < a.nq ? kOob : 0, kRsrcWord3); \
+    _Pragma("unroll") for (int k = 0; k < 2; ++k) {                                                          \
+      const uint32_t vo = ((x_tap[h_][k] >> tap) & 1u) ? x_off[h_][k] : kOob;                                \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G8_BUF + \
+                                                                                       G8_BOFF + g8_brow(h_, wid_u + 8 * k, 0) * 128), \
+                                               16, vo, 0, 0, 0);                                             \
+    }                                                                                                        \
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fh = lane >> 4;
+  bf16x8 af[4][2], bfr[2][2];
+
+  // prologue: tile 0 -> buf0 (all four halves), tile 1 -> buf1.A0 / buf1.B1 (what phases 6-7 would issue)
+  Cur c0{0, 0, 0, 0};
+  Cur c1 = advance(c0);
+  IC2_G8_ISSUE_A(0, 0, c0);
+  IC2_G8_ISSUE_B(0, 0, c0);
+  IC2_G8_ISSUE_A(1, 0, c0);
+  IC2_G8_ISSUE_B(1, 0, c0);
+  IC2_G8_ISSUE_A(0, 1, c1);
+  IC2_G8_ISSUE_B(1, 1, c1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // o-group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define IC2_G8_READ_A(buf_, qm_)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int s = 0; s < 2; ++s) af[i][s] =    \
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G8_BUF + g8_off(grp * 128 + (qm_) * 64 + i * 16 + fr, 4 * s + fh));
+#define IC2_G8_READ_B(buf_, qn_)                                                                              \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int s = 0; s < 2; ++s) bfr[j][s] =   \
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G8_BUF + G8_BOFF +                                      \
+                                       g8_off(wp_ * 64 + (qn_) * 32 + j * 16 + fr, 4 * s + fh));
+#define IC2_G8_COMPUTE(qm_, qn_, WAIT_)                                                                       \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  WAIT_;                                                                                                     \
+  __builtin_amdgcn_s_barrier();                                                                              \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                         \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  __builtin_amdgcn_s_setprio(1);                                                                             \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)               \
+      _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + i][(qn_) * 2 + j] =                      \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[(qm_) * 4 + i][(qn_) * 2 + j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);                                                                             \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  __builtin_amdgcn_s_barrier();                                                                              \
+  __builtin_amdgcn_sched_barrier(0);
+#define IC2_G8_NOWAIT (void)0
+#define IC2_G8_WAIT4 asm volatile("s_waitcnt vmcnt(4)" ::: "memory")
+
+  const int niter = (a.nq + 1) >> 1;
+  Cur cn = c1;  // tile 2i+1
+  for (int it = 0; it < niter; ++it) {
+    const Cur cA = cn;               // 2i+1
+    const Cur cB = advance(cA);      // 2i+2
+    const Cur cC = advance(cB);      // 2i+3
+    // phase 0: buf0 quadrant (0,0); restage buf1.A1 <- 2i+1
+    IC2_G8_READ_B(0, 0);
+    IC2_G8_READ_A(0, 0);
+    IC2_G8_ISSUE_A(1, 1, cA);
+    IC2_G8_COMPUTE(0, 0, IC2_G8_NOWAIT);
+    // phase 1: (0,1); buf1.B0 <- 2i+1
+    IC2_G8_READ_B(0, 1);
+    IC2_G8_ISSUE_B(0, 1, cA);
+    IC2_G8_COMPUTE(0, 1, IC2_G8_NOWAIT);
+    // phase 2: (1,1); buf0.A0 <- 2i+2
+    IC2_G8_READ_A(0, 1);
+    IC2_G8_ISSUE_A(0, 0, cB);
+    IC2_G8_COMPUTE(1, 1, IC2_G8_NOWAIT);
+    // phase 3: (1,0); buf0.B1 <- 2i+2; retire tile 2i+1 (buf1) for phases 4-7
+    IC2_G8_READ_B(0, 0);
+    IC2_G8_ISSUE_B(1, 0, cB);
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT4);
+    // phase 4: buf1 quadrant (0,0); buf0.A1 <- 2i+2
+    IC2_G8_READ_B(1, 0);
+    IC2_G8_READ_A(1, 0);
+    IC2_G8_ISSUE_A(1, 0, cB);
+    IC2_G8_COMPUTE(0, 0, IC2_G8_NOWAIT);
+    // phase 5: (0,1); buf0.B0 <- 2i+2
+    IC2_G8_READ_B(1, 1);
+    IC2_G8_ISSUE_B(0, 0, cB);
+    IC2_G8_COMPUTE(0, 1, IC2_G8_NOWAIT);
+    // phase 6: (1,1); buf1.A0 <- 2i+3
+    IC2_G8_READ_A(1, 1);
+    IC2_G8_ISSUE_A(0, 1, cC);
+    IC2_G8_COMPUTE(1, 1, IC2_G8_NOWAIT);
+    // phase 7: (1,0); buf1.B1 <- 2i+3; retire tile 2i+2 (buf0) for the next iteration
+    IC2_G8_READ_B(1, 0);
+    IC2_G8_ISSUE_B(1, 1, cC);
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT4);
+    cn = cC;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail DMAs (zero tiles) before exit
+  if (grp == 0) __builtin_amdgcn_s_barrier();       // balance the o-group-1 offset barrier
+#undef IC2_G8_ISSUE_A
+#undef IC2_G8_ISSUE_B
+#undef IC2_G8_READ_A
+#undef IC2_G8_READ_B
+#undef IC2_G8_COMPUTE
+#undef IC2_G8_NOWAIT
+#undef IC2_G8_WAIT4
+  ig_epilogue<8, 4>(a, acc, o0 + grp * 128, m0 + wp_ * 64, fr, fh);
 }
 
 template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
@@ -302,6 +550,12 @@ extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, 
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
   a.out_layout = out_layout; a.out_dtype = out_dtype;
+  static const int group = [] {
+    const char* e = getenv("IC2_IGEMM_GROUP");
+    const int g = e ? atoi(e) : 1;  // 1 = o-tiles of a p-tile side by side (measured best)
+    return g >= 1 ? g : 1;
+  }();
+  a.group = group;
   hipStream_t s = as_stream(stream);
   if (dtype == IC2_BF16) {
     // the widest o-tile the layer fills; 256-pixel tiles while the grid keeps >= 2 workgroups per CU
@@ -319,8 +573,21 @@ extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, 
     else if (cout_p % 128 == 0) tile = 3;
     else if (cout_p % 64 == 0) tile = 5;
     else tile = 2;
-    if (forced >= 1 && forced <= 5) tile = forced;
+    // the 8-phase 256 x 256 kernel wherever the o-tile is wider than 128 and K-tiles are 64 deep
+    // (its buffer descriptors address < 2 GiB per operand and its tap masks hold <= 32 taps)
+    const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && (int64_t)n * h * w_ * cin_p * 2 < (int64_t)kOob &&
+                       (int64_t)cout_p * a.K * 2 < (int64_t)kOob;
+    if (big_m && cout_p > 128 && fits8) tile = 6;  // even with 25 % padded rows (cout 192) it wins
+    if (forced >= 1 && forced <= 6) tile = forced;
+    if (tile == 6 && !fits8) tile = 1;
     switch (tile) {
+      case 6: {
+        a.tiles_o = (cout_p + 255) / 256;
+        a.nq = a.K / 64;
+        a.nblocks = (int)(ceil_div(a.M, 256) * a.tiles_o);
+        hipLaunchKernelGGL(igemm8_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+        break;
+      }
       case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, s); break;
       case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, s); break;
       case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, s); break;

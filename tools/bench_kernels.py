@@ -66,11 +66,11 @@ def main():
     env_name = "IC2_FLR_VARIANT" if kind == "flr" else "IC2_IGEMM_TILE"
     table = {}
     for v in variants:
-        # "v" or "v,p" (p = IC2_FLR_PERSIST for flr, IC2_IGEMM_SPLITK for igemm)
+        # "v" or "v,p" (p = IC2_FLR_PERSIST for flr, IC2_IGEMM_GROUP for igemm)
         parts = v.split(",")
         env = dict(os.environ, **{env_name: parts[0]})
         if len(parts) > 1:
-            env["IC2_FLR_PERSIST" if kind == "flr" else "IC2_IGEMM_SPLITK"] = parts[1]
+            env["IC2_FLR_PERSIST" if kind == "flr" else "IC2_IGEMM_GROUP"] = parts[1]
         r = subprocess.run([sys.executable, __file__, "--child", kind], env=env, capture_output=True, text=True,
                            timeout=600)
         if r.returncode != 0:

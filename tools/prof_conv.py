@@ -1,0 +1,29 @@
+"""Run one synthesis-layer implicit-GEMM conv (SG3-T-256 L8 shape by default, batch 32 bf16) a few times:
+the target for rocprofv3 --pmc passes.   python tools/prof_conv.py [cin cout size reps]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from image_compression_2_amd import _native as nv
+    cin, cout, size, reps = [int(v) for v in (sys.argv[1:] + ["512", "512", "148", "5"][len(sys.argv) - 1:])]
+    dev = torch.device("cuda", 0)
+    n = 32
+    conv = size + 2
+    x = torch.randn(n, size, size, cin, device=dev).to(torch.bfloat16)
+    w = (torch.randn(cout, 3, 3, cin, device=dev) / (9 * cin) ** 0.5).to(torch.bfloat16)
+    b = torch.zeros(cout, device=dev)
+    y = torch.empty(n, conv, conv, cout, device=dev, dtype=torch.bfloat16)
+    for _ in range(reps):
+        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(w), nv.ptr(y), nv.BF16, nv.BF16, n, size, size, cin, cout, cout,
+                3, 3, 2, conv, conv, None, nv.ptr(b), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(x))
+    torch.cuda.synchronize()
+    print("ok", float(y.float().abs().mean()))
+
+
+if __name__ == "__main__":
+    main()
