@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libic2ops.so")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 ACT_LINEAR, ACT_LRELU = 0, 1
 NHWC, NCHW = 0, 1
 
@@ -51,10 +51,12 @@ _SIGS = {
     "ic2_global_avg_pool_floats": [_I, _I, _I, _I],
     "ic2_global_avg_pool": [_P, _I, _I, _I, _I, _I, _P, _P],
     "ic2_reparameterize": [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
-    "ic2_uint8_sse": [_P, _P, _I64, _I64, _P, _P],
+    "ic2_uint8_sse_scratch_doubles": [_I64],
+    "ic2_uint8_sse": [_P, _P, _I64, _I64, _P, _P, _P],
     "ic2_resize_bilinear": [_P, _P, _I64, _I, _I, _I, _I, _P],
 }
-_RESTYPE = {"ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64}
+_RESTYPE = {"ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
+            "ic2_uint8_sse_scratch_doubles": _I64}
 
 _lib = None
 _lock = threading.Lock()
@@ -132,6 +134,8 @@ def dtype_code(dt):
         return F32
     if dt == torch.bfloat16:
         return BF16
+    if dt == torch.float16:
+        return F16
     raise TypeError(f"unsupported dtype {dt}")
 
 

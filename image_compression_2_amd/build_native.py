@@ -21,7 +21,8 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libic2ops.so")
 ARCH = os.environ.get("IC2_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wno-unused-result"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wno-unused-result",
+          *os.environ.get("IC2_EXTRA_CFLAGS", "").split()]
 
 
 def _newer(src_paths, target):
@@ -31,10 +32,15 @@ def _newer(src_paths, target):
     return any(os.path.getmtime(p) > t for p in src_paths)
 
 
+# per-file extras: the MFMA filtered-lrelu consumes every accumulator with VALU, so its MFMAs write VGPRs
+# directly instead of AGPRs (saves one v_accvgpr_read per value)
+FILE_FLAGS = {"flrelu_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _compile(src, headers, force):
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
     if force or _newer([src] + headers, obj):
-        cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+        cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

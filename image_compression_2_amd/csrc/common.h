@@ -66,7 +66,7 @@ __device__ __forceinline__ float lrelu_gain_clamp(float v, float slope, float ga
   return v;
 }
 
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // A zeroed 64-byte line in the code object: out-of-image loads read it instead of branching around
 // the load (a per-load branch makes hipcc wait vmcnt(0) per element -> serialised round trips).

@@ -43,39 +43,59 @@ __global__ void __launch_bounds__(256) nhwc_to_nchw_kernel(const T* __restrict__
 // ------------------------------------------------------------------------------------------------
 // GroupNorm statistics: stage 1 = per (n, pixel chunk) per-group partial sums (f64) written to
 // `part`; stage 2 = per (n, group) ordered sum over chunks -> mean, rstd.  Deterministic.
+// The chunk length adapts to the layer so that every layer launches >= ~2048 workgroups
+// (the 8x8 / 4x4 encoder blocks otherwise run 32 latency-bound workgroups).
 // ------------------------------------------------------------------------------------------------
-constexpr int GN_CHUNK_PIX = 256;
+__host__ __device__ inline int gn_chunk_pix(int n, int hw) {
+  const int64_t want = ceil_div((int64_t)n * hw, 2048);
+  return (int)(want < 8 ? 8 : (want > 256 ? 256 : want));
+}
+
+// two channels per thread (bf16x2 / float2 loads)
+template <typename T> __device__ __forceinline__ float2 ld2(const T* p);
+template <> __device__ __forceinline__ float2 ld2<float>(const float* p) { return *reinterpret_cast<const float2*>(p); }
+template <> __device__ __forceinline__ float2 ld2<bf16_t>(const bf16_t* p) {
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y, int hw, int c_p, int c, int groups,
-                                                         int nchunks, double* __restrict__ part) {
-  // threads own channels (coalesced NHWC reads): thread t -> channel t % CT (+ k*256 when c_p > 256),
-  // pixel phase t / CT; per-thread fp32 sums over <= 256 pixels, then a fixed-order f64 group reduction
-  extern __shared__ __attribute__((aligned(16))) double sred[];  // [2][max(256, c_p)]
+                                                         int nchunks, int chunk_pix, double* __restrict__ part) {
+  // thread t -> channel pair t % CT (+ k*CT*... when c_p > 512), pixel phase t / CT; per-thread fp32
+  // sums over <= chunk_pix / PS pixels, then a fixed-order f64 group reduction
+  extern __shared__ __attribute__((aligned(16))) double sred[];  // [2][max(512, c_p)]
   const int chunk = blockIdx.x % nchunks;
   const int nn = blockIdx.x / nchunks;
   const int cpg = c / groups;
-  const int p0 = chunk * GN_CHUNK_PIX;
-  const int p1 = min(hw, p0 + GN_CHUNK_PIX);
+  const int p0 = chunk * chunk_pix;
+  const int p1 = min(hw, p0 + chunk_pix);
   const T* yb = y + (int64_t)nn * hw * c_p;
-  const int CT = c_p < 256 ? c_p : 256;  // channels covered per pass
-  const int PS = 256 / CT;               // pixel phases
-  const int ch0 = threadIdx.x % CT;
+  const int npair = c_p >> 1;
+  const int CT = npair < 256 ? npair : 256;  // channel pairs covered per pass
+  const int PS = 256 / CT;                   // pixel phases
+  const int cp0 = threadIdx.x % CT;
   const int pp = threadIdx.x / CT;
-  const int nslots = c_p < 256 ? 256 : c_p;
+  const int nslots = c_p < 512 ? 512 : c_p;
   double* ssum = sred;
   double* ssq = sred + nslots;
   if (pp < PS) {
-    for (int cc = ch0; cc < c_p; cc += 256) {
-      float s = 0.f, q = 0.f;
+    for (int cq = cp0; cq < npair; cq += 256) {
+      float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+#pragma unroll 8
       for (int p = p0 + pp; p < p1; p += PS) {
-        const float v = ld(yb + (int64_t)p * c_p + cc);
-        s += v;
-        q += v * v;
+        const float2 v = ld2(yb + (int64_t)p * c_p + 2 * cq);
+        s0 += v.x;
+        q0 += v.x * v.x;
+        s1 += v.y;
+        q1 += v.y * v.y;
       }
-      const int slot = c_p < 256 ? threadIdx.x : cc;
-      ssum[slot] = s;
-      ssq[slot] = q;
+      // slot = (phase, channel) for c_p < 512, else channel
+      const int slot = c_p < 512 ? pp * c_p + 2 * cq : 2 * cq;
+      ssum[slot] = s0;
+      ssq[slot] = q0;
+      ssum[slot + 1] = s1;
+      ssq[slot + 1] = q1;
     }
   }
   __syncthreads();
@@ -83,10 +103,10 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y
     double s = 0.0, q = 0.0;
     for (int k = 0; k < cpg; ++k) {
       const int cc = g * cpg + k;
-      if (c_p < 256) {
+      if (c_p < 512) {
         for (int ph = 0; ph < PS; ++ph) {
-          s += ssum[ph * CT + cc];
-          q += ssq[ph * CT + cc];
+          s += ssum[ph * c_p + cc];
+          q += ssq[ph * c_p + cc];
         }
       } else {
         s += ssum[cc];
@@ -117,8 +137,36 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const double* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// GroupNorm apply + lrelu (+ 2x2 average pool); 4 channels per thread
+// GroupNorm apply + lrelu (+ 2x2 average pool); 8 channels (one 16-B bf16 / 2x16-B f32 vector) per thread
 // ------------------------------------------------------------------------------------------------
+template <typename T> __device__ __forceinline__ void ld8(const T* p, float (&v)[8]);
+template <> __device__ __forceinline__ void ld8<float>(const float* p, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> __device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void st8(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void st8<float>(float* p, const float (&v)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <> __device__ __forceinline__ void st8<bf16_t>(bf16_t* p, const float (&v)[8]) {
+  uint4 u;
+  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y, TO* __restrict__ out, int n, int h,
                                                        int w, int c_p, int c, int groups,
@@ -126,41 +174,54 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float slope, int pool) {
   const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
-  const int cq = c_p / 4;
-  const int64_t total = (int64_t)n * oh * ow * cq;
+  const int c8 = c_p / 8;
+  const int64_t total = (int64_t)n * oh * ow * c8;
   const int cpg = c / groups;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int ch0 = (int)(e % cq) * 4;
-    const int64_t pix = e / cq;
+    const int ch0 = (int)(e % c8) * 8;
+    const int64_t pix = e / c8;
     const int ox = (int)(pix % ow);
     const int oy = (int)((pix / ow) % oh);
     const int nn = (int)(pix / ((int64_t)ow * oh));
-    float res[4];
+    float mu[8], sc[8], sh[8];  // t = (v - mean) * (rstd * gamma) + beta
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int ch = ch0 + k;
-      res[k] = 0.f;
-      if (ch >= c) continue;
-      const int g = ch / cpg;
-      const float mean = stats[((int64_t)nn * groups + g) * 2 + 0];
-      const float rstd = stats[((int64_t)nn * groups + g) * 2 + 1];
-      const float ga = gamma[ch], be = beta[ch];
-      auto f = [&](int yy, int xx) {
-        const float v = ld(y + (((int64_t)nn * h + yy) * w + xx) * c_p + ch);
-        const float t = (v - mean) * rstd * ga + be;
-        return t < 0.f ? t * slope : t;
-      };
-      if (pool) {
-        const float a0 = f(2 * oy, 2 * ox), a1 = f(2 * oy, 2 * ox + 1);
-        const float a2 = f(2 * oy + 1, 2 * ox), a3 = f(2 * oy + 1, 2 * ox + 1);
-        res[k] = (((a0 + a1) + a2) + a3) / 4.f;
+      if (ch < c) {
+        const int g = ch / cpg;
+        const float mean = stats[((int64_t)nn * groups + g) * 2 + 0];
+        const float rstd = stats[((int64_t)nn * groups + g) * 2 + 1];
+        mu[k] = mean;
+        sc[k] = rstd * gamma[ch];
+        sh[k] = beta[ch];
       } else {
-        res[k] = f(oy, ox);
+        mu[k] = 0.f;
+        sc[k] = 0.f;
+        sh[k] = 0.f;
       }
     }
-    TO* o = out + pix * c_p + ch0;
+    float res[8];
+    auto f = [&](int yy, int xx, float (&r)[8], bool accum) {
+      float v[8];
+      ld8(y + (((int64_t)nn * h + yy) * w + xx) * c_p + ch0, v);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st(o + k, res[k]);
+      for (int k = 0; k < 8; ++k) {
+        float t = (v[k] - mu[k]) * sc[k] + sh[k];
+        t = t < 0.f ? t * slope : t;
+        r[k] = accum ? r[k] + t : t;
+      }
+    };
+    if (pool) {
+      f(2 * oy, 2 * ox, res, false);
+      f(2 * oy, 2 * ox + 1, res, true);
+      f(2 * oy + 1, 2 * ox, res, true);
+      f(2 * oy + 1, 2 * ox + 1, res, true);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) res[k] = res[k] / 4.f;
+    } else {
+      f(oy, ox, res, false);
+    }
+    st8(out + pix * c_p + ch0, res);
   }
 }
 
@@ -223,22 +284,47 @@ __device__ __forceinline__ int to_u8(float v) {
   return (int)(t * 255.f);  // truncation, as numpy astype(np.uint8) on [0, 255]
 }
 
-__global__ void __launch_bounds__(256) uint8_sse_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                        int64_t per_img, double* __restrict__ out) {
-  __shared__ double red[256];
-  const int64_t base = (int64_t)blockIdx.x * per_img;
+// stage 1: per (image, chunk) partial sums (each thread: float4 loads, exact integer squares summed in
+// f64); stage 2: per image ordered sum over the chunks.  Deterministic, no atomics.
+constexpr int SSE_CHUNKS = 64;
+
+__global__ void __launch_bounds__(256) uint8_sse_partial_kernel(const float* __restrict__ a,
+                                                                const float* __restrict__ b, int64_t per_img,
+                                                                int vec, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int chunk = blockIdx.x, img = blockIdx.y;
+  const int64_t len = ceil_div(ceil_div(per_img, SSE_CHUNKS), 4) * 4;
+  const int64_t i0 = (int64_t)chunk * len, i1 = min(per_img, i0 + len);
+  const float* pa = a + (int64_t)img * per_img;
+  const float* pb = b + (int64_t)img * per_img;
   double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < per_img; i += 256) {
-    const int d = to_u8(a[base + i]) - to_u8(b[base + i]);
-    acc += (double)(d * d);
+  if (vec) {
+    for (int64_t i = i0 + 4 * threadIdx.x; i < i1; i += 1024) {
+      const float4 u = *reinterpret_cast<const float4*>(pa + i), v = *reinterpret_cast<const float4*>(pb + i);
+      const int d0 = to_u8(u.x) - to_u8(v.x), d1 = to_u8(u.y) - to_u8(v.y);
+      const int d2 = to_u8(u.z) - to_u8(v.z), d3 = to_u8(u.w) - to_u8(v.w);
+      acc += (double)(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+    }
+  } else {
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+      const int d = to_u8(pa[i]) - to_u8(pb[i]);
+      acc += (double)(d * d);
+    }
   }
-  red[threadIdx.x] = acc;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+  if (threadIdx.x == 0) part[(int64_t)img * SSE_CHUNKS + chunk] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void __launch_bounds__(256) uint8_sse_finalize_kernel(const double* __restrict__ part, int64_t n_img,
+                                                                 double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_img) return;
+  double s = 0.0;
+  for (int k = 0; k < SSE_CHUNKS; ++k) s += part[i * SSE_CHUNKS + k];
+  out[i] = s;
 }
 
 // F.interpolate(bilinear, align_corners=False): src = max(0, (dst + 0.5) * in/out - 0.5)
@@ -301,25 +387,27 @@ extern "C" int ic2_nhwc_to_nchw(const void* x, int dtype, float* y, int n, int c
 
 extern "C" int64_t ic2_group_norm_stats_floats(int n, int hw, int groups) {
   const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
-  return stats_floats + (int64_t)n * groups * ceil_div(hw, GN_CHUNK_PIX) * 2 * 2;
+  return stats_floats + (int64_t)n * groups * ceil_div(hw, gn_chunk_pix(n, hw)) * 2 * 2;
 }
 
 extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c, int groups, float eps,
                                     float* stats_out, void* stream) {
   IC2_CHECK_ARG(y && stats_out && n > 0 && hw > 0 && c > 0 && groups > 0 && c % groups == 0 && c_p >= c,
                 "group_norm_stats: bad arguments");
-  const int nchunks = (int)ceil_div(hw, GN_CHUNK_PIX);
+  IC2_CHECK_ARG(c_p % 2 == 0, "group_norm_stats: c_p must be even");
+  const int chunk_pix = gn_chunk_pix(n, hw);
+  const int nchunks = (int)ceil_div(hw, chunk_pix);
   // partials live right after the stats (8-byte aligned)
   const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
   double* part = reinterpret_cast<double*>(stats_out + stats_floats);
   hipStream_t s = as_stream(stream);
-  const size_t lds = 2 * (size_t)(c_p < 256 ? 256 : c_p) * sizeof(double);
+  const size_t lds = 2 * (size_t)(c_p < 512 ? 512 : c_p) * sizeof(double);
   if (dtype == IC2_F32)
     hipLaunchKernelGGL(gn_partial_kernel<float>, dim3(n * nchunks), dim3(256), lds, s, (const float*)y, hw, c_p, c,
-                       groups, nchunks, part);
+                       groups, nchunks, chunk_pix, part);
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(n * nchunks), dim3(256), lds, s, (const bf16_t*)y, hw, c_p, c,
-                       groups, nchunks, part);
+                       groups, nchunks, chunk_pix, part);
   else
     IC2_CHECK_ARG(false, "group_norm_stats: bad dtype");
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)ceil_div(n * groups, 256)), dim3(256), 0, s, part, n * groups,
@@ -331,11 +419,11 @@ extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int
 extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p,
                                  int c, int groups, const float* stats, const float* gamma, const float* beta,
                                  float slope, int pool, void* stream) {
-  IC2_CHECK_ARG(y && out && stats && gamma && beta && n > 0 && h > 0 && w > 0 && c_p % 4 == 0 && c <= c_p,
+  IC2_CHECK_ARG(y && out && stats && gamma && beta && n > 0 && h > 0 && w > 0 && c_p % 8 == 0 && c <= c_p,
                 "gn_lrelu_pool: bad arguments");
   IC2_CHECK_ARG(!pool || (h >= 2 && w >= 2), "gn_lrelu_pool: pooling needs H, W >= 2");
   const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
-  const int64_t total = (int64_t)n * oh * ow * (c_p / 4);
+  const int64_t total = (int64_t)n * oh * ow * (c_p / 8);
   hipStream_t s = as_stream(stream);
 #define IC2_GN_LAUNCH(TI, TO)                                                                                     \
   hipLaunchKernelGGL((gn_apply_kernel<TI, TO>), dim3(grid_1d(total)), dim3(256), 0, s, (const TI*)y, (TO*)out, n, h, \
@@ -383,10 +471,18 @@ extern "C" int ic2_reparameterize(const float* params, const float* eps, int n, 
   return IC2_OK;
 }
 
+extern "C" int64_t ic2_uint8_sse_scratch_doubles(int64_t n_img) { return n_img * SSE_CHUNKS; }
+
 extern "C" int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img, double* sse_out,
-                             void* stream) {
-  IC2_CHECK_ARG(a && b && sse_out && n_img > 0 && per_img > 0 && n_img < (1LL << 31), "uint8_sse: bad arguments");
-  hipLaunchKernelGGL(uint8_sse_kernel, dim3((unsigned)n_img), dim3(256), 0, as_stream(stream), a, b, per_img, sse_out);
+                             double* scratch, void* stream) {
+  IC2_CHECK_ARG(a && b && sse_out && scratch && n_img > 0 && per_img > 0 && n_img < 65536,
+                "uint8_sse: bad arguments");
+  hipStream_t s = as_stream(stream);
+  const int vec = per_img % 4 == 0 && ((uintptr_t)a | (uintptr_t)b) % 16 == 0;
+  hipLaunchKernelGGL(uint8_sse_partial_kernel, dim3(SSE_CHUNKS, (unsigned)n_img), dim3(256), 0, s, a, b, per_img, vec,
+                     scratch);
+  hipLaunchKernelGGL(uint8_sse_finalize_kernel, dim3((unsigned)ceil_div(n_img, 256)), dim3(256), 0, s, scratch, n_img,
+                     sse_out);
   IC2_CHECK_LAUNCH("uint8_sse");
   return IC2_OK;
 }

@@ -1,0 +1,30 @@
+// Shared between the fused filtered-lrelu kernels (flrelu.hip: VALU, every dtype/layout;
+// flrelu_mfma.hip: the bf16 NHWC synthesis path on MFMA).
+#pragma once
+#include "common.h"
+
+namespace ic2 {
+
+struct FlrArgs {
+  const void* x;
+  void* y;
+  const float* bias;
+  const float* post_scale;  // [n][c_p] or null
+  int64_t xsn, xsy, xsx, xsc;  // input strides (elements)
+  int64_t ysn, ysy, ysx, ysc;  // output strides
+  int c, c_p;                   // valid channels, post_scale row stride
+  int in_h, in_w, out_h, out_w;
+  int py0, px0;                 // leading padding
+  int tiles_x, tiles_y, cblocks, nimg;
+  float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
+  float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
+  float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
+  float gd[12];  // flipped (unless flip_filter)
+};
+
+// NHWC, f16 (in_f16) or bf16 input, bf16 output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
+// bias (folded into the producer).  Sets tiles/cblocks itself.  Returns IC2_E_UNSUPPORTED when the
+// configuration has no MFMA instance.
+int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, int delta, int n, hipStream_t s);
+
+}  // namespace ic2

@@ -13,7 +13,7 @@
 //   stage 3  vertical down-FIR : LDS column -> * post_scale -> global
 // Filters are separable 1-D taps (the StyleGAN3-T configuration).  Zero padding / negative
 // padding (crop) is exact: input samples outside [0, L) are zero, as in the reference.
-#include "common.h"
+#include "flrelu.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -21,23 +21,6 @@
 namespace ic2 {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
-
-struct FlrArgs {
-  const void* x;
-  void* y;
-  const float* bias;
-  const float* post_scale;  // [n][c_p] or null
-  int64_t xsn, xsy, xsx, xsc;  // input strides (elements)
-  int64_t ysn, ysy, ysx, ysc;  // output strides
-  int c, c_p;                   // valid channels, post_scale row stride
-  int in_h, in_w, out_h, out_w;
-  int py0, px0;                 // leading padding
-  int tiles_x, tiles_y, cblocks, nimg;
-  float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
-  float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
-  float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
-  float gd[12];  // flipped (unless flip_filter)
-};
 
 template <int U, int D, int TU, int TD, int TOY, int TOX>
 struct FlrGeom {
@@ -356,6 +339,33 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   a.c_p = c_p;
   a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w;
   a.py0 = py0; a.px0 = px0;
+  hipStream_t s = as_stream(stream);
+  // bf16 NHWC (the synthesis throughput path): the MFMA formulation (flrelu_mfma.hip) unless
+  // IC2_FLR_MFMA=0 asks for the VALU kernel below
+  static const bool use_mfma = [] {
+    const char* e = getenv("IC2_FLR_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  // f16 input (the synthesis conv epilogue's output) exists only for the MFMA formulation
+  const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) && dtype_out == IC2_BF16 && b == nullptr;
+  if ((use_mfma || dtype_in == IC2_F16) && mfma_ok) {
+    for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
+    for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;
+    for (int t = 0; t < fu_taps; ++t) a.gu[t] = (fu ? (flip ? fu[t] : fu[fu_taps - 1 - t]) : 1.f) * (float)up;
+    for (int t = 0; t < fd_taps; ++t) a.gd[t] = fd ? (flip ? fd[t] : fd[fd_taps - 1 - t]) : 1.f;
+    for (int t = 0; t < 12; ++t) a.gdg[t] = a.gd[t] * gain;
+    a.slope = slope;
+    a.lim = clamp >= 0.f ? clamp / gain : INFINITY;
+    if (flrelu_mfma_launch(a, dtype_in == IC2_F16, up, down, fu_taps, fd_taps, dx, n, s) == IC2_OK) {
+      IC2_CHECK_LAUNCH(name);
+      return IC2_OK;
+    }
+  }
+  if (dtype_in == IC2_F16) {
+    set_error("%s: f16 input needs the MFMA instance (NHWC, bf16 out, no bias, up 2/4 with 6*up taps, down 2 / 12 taps)",
+              name);
+    return IC2_E_UNSUPPORTED;
+  }
   const int geom = flr_pick(chlast && dtype_in == IC2_BF16 && dtype_out == IC2_BF16, up);
   const FlrGeomSel fv = kFlrGeoms[geom];
   a.tiles_x = (int)ceil_div(out_w, fv.tox);
@@ -372,7 +382,6 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   for (int t = 0; t < 12; ++t) a.gdg[t] = a.gd[t] * gain;
   const int64_t grid = (int64_t)n * a.tiles_y * a.tiles_x * a.cblocks;
   IC2_CHECK_ARG(grid < (1LL << 31), "%s: grid too large", name);
-  hipStream_t s = as_stream(stream);
   int rc;
   if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16)
     rc = chlast ? launch_cfg<bf16_t, bf16_t, true>(a, up, down, fu_taps, fd_taps, dx, geom, (int)grid, s)

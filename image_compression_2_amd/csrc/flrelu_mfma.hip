@@ -1,0 +1,371 @@
+// Fused filtered leaky-ReLU on the matrix cores: the bf16 NHWC synthesis path of
+// SynthesisLayer.forward [SG3-public filtered_lrelu: bias_act -> upfirdn2d(fu, up) -> lrelu*gain, clamp
+// -> upfirdn2d(fd, down)], called for every layer of G.synthesis (/root/reference/stylegan3_hvae_full.py:274,329).
+//
+// Every separable FIR pass is a small banded matrix applied along one axis, and the FIR never mixes
+// channels, so each pass is an MFMA with 16 channels on one side and 16 positions along the filtered
+// axis on the other:
+//   vertical up     V^T[c][ky] = X^T[c][jy] . Gu^T[jy][ky]      (A from LDS by transposed read)
+//   horizontal up   U[kx][c]   = Gu[kx][jx] . V[jx][c]          (B from LDS by transposed read)
+//   activation      lrelu(U) * gain, clamp  (f32, on the accumulator)
+//   horizontal down D^T[c][ox] = act(U)^T[c][kx] . GdT[kx][ox]  (the accumulator IS the A operand)
+//   vertical down   O^T[c][oy] = D^T[c][ky] . GdT[ky][oy]       (A from LDS by transposed read)
+// The filter matrices are built once per workgroup into registers (bf16 taps); 16x16x16 MFMAs for the
+// up passes (a 16-output band spans <= 14 inputs), 16x16x32 where K can be filled (horizontal down).
+// A tile = one sample x one 16x16 output tile x 16 channels; 4 waves split columns / rows / output
+// columns of each 16-row grid block; the up-sampled grid exists only 16 rows at a time in LDS.  Persistent
+// workgroups loop over tiles and prefetch the next tile's input (LDS-DMA) while finishing the current one.
+#include "flrelu.h"
+
+namespace ic2 {
+
+typedef _Float16 fm_h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 fm_h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 fm_h8 __attribute__((ext_vector_type(8)));
+typedef short fm_s4 __attribute__((ext_vector_type(4)));
+typedef float fm_f4 __attribute__((ext_vector_type(4)));
+typedef float fm_f2 __attribute__((ext_vector_type(2)));
+
+constexpr int FM_TAPS = 276;
+
+template <int U>
+struct FmGeom {
+  static constexpr int TU = 6 * U, TD = 12;
+  static constexpr int TO = 16;                        // output tile side
+  static constexpr int RA = (TO - 1) * 2 + TD;         // 42 lrelu-grid rows / columns per tile
+  static constexpr int NIN = (RA + TU - 2) / U + 1;    // 27 (up 2) / 17 (up 4) input rows / columns
+  static constexpr int NB = (RA + 15) / 16;            // 3 grid blocks of 16
+  // LDS images (dwords); pitches chosen for conflict-free transposed reads / b64 writes
+  static constexpr int IN_PITCH = NIN * 8;             // [jy][x][16 ch]: NIN odd -> 8 rows hit 8 bank groups
+  // allocated in whole 1-KB LDS-DMA instructions: the last one's tail lanes (zeros) must not spill into V
+  static constexpr int IN_DW = (NIN * NIN * 2 + 63) / 64 * 256;
+  static constexpr int V_PITCH = NIN * 8 + 2;          // [ky][x][16 ch]: 16 rows of b64 writes hit 16 bank pairs
+  static constexpr int V_DW = 16 * V_PITCH;
+  static constexpr int D_XP = 10;                      // [ky][ox][16 ch], ox pitch 10 dwords
+  static constexpr int D_PITCH = 16 * D_XP + 8;        // 168 = 40 mod 64: 8 rows hit 8 bank groups
+  static constexpr int D_DW = 16 * D_PITCH;
+  static constexpr int LDS_DW = IN_DW + V_DW + D_DW + FM_TAPS;
+  static_assert(NIN % 2 == 1 && NIN >= 16, "input image width must be odd and cover a 16-wide window");
+};
+
+// first input sample feeding grid position i (polyphase), then clipped so a 16-wide window stays
+// inside the NIN-sample image (taps outside the band are zero, so a window shifted back is exact)
+template <int U, int DELTA, int NIN>
+__device__ constexpr int fm_win(int i) {
+  const int j = i < DELTA ? 0 : (i - DELTA + U - 1) / U;
+  return j < NIN - 16 ? j : NIN - 16;
+}
+
+#ifdef IC2_FM_NOPS
+#define FM_SETTLE(v) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(v))
+#else
+#define FM_SETTLE(v) (void)0
+#endif
+
+__device__ __forceinline__ fm_s4 fm_tr_read(const uint32_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) fm_s4*)p);
+}
+
+// f32 -> f16 pairs (v_cvt_pk_f16_f32, round to nearest even)
+__device__ __forceinline__ uint32_t fm_h2u(float a, float b) {
+  return __builtin_bit_cast(uint32_t, fm_h2{(_Float16)a, (_Float16)b});
+}
+__device__ __forceinline__ uint2 fm_pack4(float a, float b, float c, float d) {
+  return make_uint2(fm_h2u(a, b), fm_h2u(c, d));
+}
+__device__ __forceinline__ fm_h4 fm_h4_of(uint2 u) { return __builtin_bit_cast(fm_h4, u); }
+__device__ __forceinline__ fm_h8 fm_h8_of(uint2 lo, uint2 hi) {
+  return __builtin_bit_cast(fm_h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+// bf16 pair -> f16 pair, saturated to the f16 range (a pre-activation beyond +-65504 ends up clamped
+// by the activation anyway)
+__device__ __forceinline__ uint32_t fm_bf2_to_h2(uint32_t v) {
+  const float lo = __builtin_amdgcn_fmed3f(__uint_as_float(v << 16), -65504.f, 65504.f);
+  const float hi = __builtin_amdgcn_fmed3f(__uint_as_float(v & 0xffff0000u), -65504.f, 65504.f);
+  return fm_h2u(lo, hi);
+}
+
+// lrelu + clamp on a pair in 5 instructions (gain folded into the horizontal down taps):
+// for 0 <= slope <= 1, med3(v, slope*v, lim) is lrelu(v) clamped from above wherever |slope*v| <= lim, and
+// the outer med3 finishes the clamp for the rest (no fmaxf: it would cost a canonicalizing max per value)
+__device__ __forceinline__ fm_f2 fm_act2(fm_f2 v, float slope, float lim) {
+  const fm_f2 sv = v * slope;
+  fm_f2 r;
+  r.x = __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(v.x, sv.x, lim), -lim, lim);
+  r.y = __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(v.y, sv.y, lim), -lim, lim);
+  return r;
+}
+
+__device__ __forceinline__ int fm_xcd_remap(int b, int nblocks) {
+  const int xcd = b & 7, loc = b >> 3;
+  const int q8 = nblocks >> 3, r8 = nblocks & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+}
+
+#ifdef IC2_FM_DEBUG
+// diagnostic build only: workgroup 0 dumps its LDS images (input, V and D of grid block 0)
+__device__ uint32_t g_fm_dbg[3][8192];
+extern "C" int ic2_fm_debug_fetch(uint32_t* host, int which) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fm_dbg), 8192 * 4, (size_t)which * 8192 * 4, hipMemcpyDeviceToHost);
+}
+#define FM_DUMP(which, ptr, ndw) \
+  if (blockIdx.x == 0) for (int i_ = tid; i_ < (ndw); i_ += 256) g_fm_dbg[which][i_] = (ptr)[i_];
+#else
+#define FM_DUMP(which, ptr, ndw) (void)0
+#endif
+
+template <int U, int DELTA, bool IN_F16>
+__global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles) {
+  using G = FmGeom<U>;
+  constexpr int NIN = G::NIN, NCH = NIN * NIN * 2;  // input pixels x 16-B halves
+  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW];
+  uint32_t* const in_img = lds;
+  uint32_t* const v_img = lds + G::IN_DW;
+  uint32_t* const d_img = v_img + G::V_DW;
+  float* const taps = reinterpret_cast<float*>(d_img + G::D_DW);  // FM_TAPS floats, layout below
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;  // this lane's (row, 4-column group) in a transposed read
+
+  // tap tables with zero guard bands, so every per-lane filter-matrix entry below is a branch-free read
+  // (tap ranges: up [-43, 63], down [-30, 47]): gu at [48, 72) of [0, 116), gd at [148, 160) of [116, 196),
+  // gdg (gain folded) at [228, 240) of [196, 276)
+  for (int i = tid; i < FM_TAPS; i += 256) {
+    float v = 0.f;
+    if (i >= 48 && i < 72) v = a.gu[i - 48];
+    else if (i >= 148 && i < 160) v = a.gd[i - 148];
+    else if (i >= 228 && i < 240) v = a.gdg[i - 228];
+    taps[i] = v;
+  }
+
+  // persistent: this workgroup runs tiles slot, slot + gridDim.x, ...  Logical tiles run channel block
+  // fastest and consecutive slots share an XCD, so the channel blocks of one tile (16 channels = 32 B of
+  // each 128-B line of the input) are fetched once into that XCD's L2.
+  const int slot = fm_xcd_remap(blockIdx.x, gridDim.x);
+  const uint16_t* xin = reinterpret_cast<const uint16_t*>(a.x);
+  auto tile_geom = [&](int t, int& n, int& oy0, int& ox0, int& c0) {
+    const int cb = t % a.cblocks;
+    t /= a.cblocks;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    n = t / a.tiles_y;
+    oy0 = ty * 16;
+    ox0 = tx * 16;
+    c0 = cb * 16;
+  };
+  // input tile -> in_img[jy][x][16 ch] (zeros outside the image).  The image is dense (pixel p at 32 B * p),
+  // i.e. lane-linear in (pixel, 16-B half): f16 input goes to LDS by LDS-DMA, asynchronously.
+  auto chunk_src = [&](int e, int n, int sy0, int sx0, int c0) -> const void* {
+    const int pix = e >> 1, half = e & 1;
+    const int jy = pix / NIN, x = pix - jy * NIN;
+    const int iy = sy0 + jy, ix = sx0 + x;
+    const bool ok = e < NCH && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
+    const uint16_t* src = xin + (((int64_t)n * a.in_h + iy) * a.in_w + ix) * a.c_p + c0 + half * 8;
+    return ok ? (const void*)src : zero_line();
+  };
+  auto load_tile = [&](int t) {
+    int n, oy0, ox0, c0;
+    tile_geom(t, n, oy0, ox0, c0);
+    const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
+    if constexpr (IN_F16) {
+      for (int k = wave; k * 64 < NCH; k += 4)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)chunk_src(k * 64 + lane, n, sy0,
+                                                                                                   sx0, c0),
+                                         (__attribute__((address_space(3))) void*)(in_img + k * 256), 16, 0, 0);
+    } else {
+      constexpr int PER = (NCH + 255) / 256;
+      uint4 v[PER];
+#pragma unroll
+      for (int r = 0; r < PER; ++r)  // every load in flight before the first conversion
+        v[r] = *reinterpret_cast<const uint4*>(chunk_src(tid + 256 * r, n, sy0, sx0, c0));
+#pragma unroll
+      for (int r = 0; r < PER; ++r) {
+        const int e = tid + 256 * r;
+        if (e < NCH)
+          *reinterpret_cast<uint4*>(in_img + e * 4) =
+              make_uint4(fm_bf2_to_h2(v[r].x), fm_bf2_to_h2(v[r].y), fm_bf2_to_h2(v[r].z), fm_bf2_to_h2(v[r].w));
+      }
+    }
+  };
+  if (IN_F16 && slot < ntiles) load_tile(slot);
+  __syncthreads();  // taps
+
+  // ---- filter matrices (f16: 11-bit taps; bf16 taps cost 5e-3 mean relative error on the critically
+  // sampled layers) in registers, once per workgroup
+  // gmat[t]: Gu[16t + li][win(16t) + 4g + j]  (B of the vertical pass, A of the horizontal pass)
+  fm_h4 gmat[G::NB];
+#pragma unroll
+  for (int t = 0; t < G::NB; ++t) {
+    const int w0 = fm_win<U, DELTA, NIN>(16 * t);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = U * (w0 + 4 * g + j) + DELTA - (16 * t + li);
+      v[j] = taps[48 + tap];
+    }
+    gmat[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  // horizontal down (gain folded): GdT[kx][ox = li]; x32 operands over kx blocks (0,1) and (2, zero)
+  fm_h8 gdh01, gdh2;
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kx = (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+      v[j] = taps[228 + kx - 2 * li];
+    }
+    gdh01 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[228 + 32 + 4 * g + j - 2 * li];
+    gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), make_uint2(0u, 0u));
+  }
+  // vertical down: GdT[ky = 16b + 4g + j][oy = li]
+  fm_h4 gdv[G::NB];
+#pragma unroll
+  for (int b = 0; b < G::NB; ++b) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[148 + 16 * b + 4 * g + j - 2 * li];
+    gdv[b] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  const float slope = a.slope, lim = a.lim;
+  bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
+
+  for (int t = slot; t < ntiles; t += gridDim.x) {
+    int n, oy0, ox0, c0;
+    tile_geom(t, n, oy0, ox0, c0);
+    if constexpr (!IN_F16) load_tile(t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA (and last tile's stores)
+    __syncthreads();                                   // everyone's; and the previous tile fully consumed
+    FM_DUMP(0, in_img, G::IN_DW);
+
+    fm_f4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = fm_f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int b = 0; b < G::NB; ++b) {
+      // ---- vertical up: V^T[c][ky] for the 16 grid rows of block b, every input column.  Fixed trip
+      // count (unrolled, so consecutive columns' MFMA latencies overlap); the tail columns past NIN
+      // repeat column NIN-1 (identical bytes to the same place)
+      {
+        const int w0 = fm_win<U, DELTA, NIN>(16 * b);
+#pragma unroll
+        for (int i = 0; i < (NIN + 3) / 4; ++i) {
+          const int x = min(wave + 4 * i, NIN - 1);
+          const fm_s4 xa = fm_tr_read(in_img + (w0 + 4 * g + tq) * G::IN_PITCH + x * 8 + 2 * tp);
+          fm_f4 vt = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa), gmat[b],
+                                                           fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          FM_SETTLE(vt);
+          *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) = fm_pack4(vt[0], vt[1], vt[2], vt[3]);
+        }
+      }
+      __syncthreads();
+      if (b == 0) FM_DUMP(1, v_img, G::V_DW);
+      // the input image is dead after the last vertical pass: prefetch the next tile behind the rest
+      if (IN_F16 && b == G::NB - 1 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
+      // ---- horizontal: up, activation, down, for this wave's 4 grid rows of the block (the rows past RA in
+      // the last block too: finite, and weighted by zero in the vertical down; no branch, so the rows'
+      // MFMA chains interleave)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int kyl = wave + 4 * rr;
+        fm_h4 au[G::NB];
+#pragma unroll
+        for (int tt = 0; tt < G::NB; ++tt) {
+          const int w0 = fm_win<U, DELTA, NIN>(16 * tt);
+          const fm_s4 vb = fm_tr_read(v_img + kyl * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
+          fm_f4 u = __builtin_amdgcn_mfma_f32_16x16x16f16(gmat[tt], __builtin_bit_cast(fm_h4, vb),
+                                                          fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          FM_SETTLE(u);
+          const fm_f2 p0 = fm_act2(fm_f2{u[0], u[1]}, slope, lim);
+          const fm_f2 p1 = fm_act2(fm_f2{u[2], u[3]}, slope, lim);
+          au[tt] = fm_h4_of(fm_pack4(p0.x, p0.y, p1.x, p1.y));
+        }
+        const uint2 a0 = __builtin_bit_cast(uint2, au[0]), a1 = __builtin_bit_cast(uint2, au[1]);
+        fm_f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a0, a1), gdh01, fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // block 2 as a second 16x16x32 with a zero upper half: a 16x16x16 accumulating onto the 16x16x32's
+        // result one instruction later reads stale rows 0-1 of the accumulator (mixed-shape srcC hazard)
+        const uint2 a2 = __builtin_bit_cast(uint2, au[2]);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a2, make_uint2(0u, 0u)), gdh2, d, 0, 0, 0);
+        FM_SETTLE(d);
+        *reinterpret_cast<uint2*>(d_img + kyl * G::D_PITCH + li * G::D_XP + 2 * g) = fm_pack4(d[0], d[1], d[2], d[3]);
+      }
+      __syncthreads();
+      if (b == 0) FM_DUMP(2, d_img, G::D_DW);
+      // ---- vertical down: accumulate block b's 16 grid rows into this wave's 4 output columns
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ox = wave + 4 * i;
+        const fm_s4 da = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + ox * G::D_XP + 2 * tp);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da), gdv[b], acc[i], 0, 0, 0);
+      }
+    }
+
+    // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox)
+    float ps[4] = {1.f, 1.f, 1.f, 1.f};
+    if (a.post_scale) {
+      const float4 p = *reinterpret_cast<const float4*>(a.post_scale + (int64_t)n * a.c_p + c0 + 4 * g);
+      ps[0] = p.x; ps[1] = p.y; ps[2] = p.z; ps[3] = p.w;
+    }
+    const int gy = oy0 + li;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gx = ox0 + wave + 4 * i;
+      if (gy < a.out_h && gx < a.out_w) {
+        const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
+                                   (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
+        *reinterpret_cast<uint2*>(yout + (((int64_t)n * a.out_h + gy) * a.out_w + gx) * a.c_p + c0 + 4 * g) = v;
+      }
+    }
+  }
+}
+
+template <int U, int DELTA, bool IN_F16>
+static void fm_launch_one(const FlrArgs& a, int ntiles, hipStream_t s) {
+  // persistent grid: every CU filled to the kernel's occupancy, capped by the tile count
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma_kernel<U, DELTA, IN_F16>, 256, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL((flrelu_mfma_kernel<U, DELTA, IN_F16>), dim3((unsigned)grid), dim3(256), 0, s, a, ntiles);
+}
+
+template <bool IN_F16>
+static void fm_launch(const FlrArgs& a, int up, int delta, int ntiles, hipStream_t s) {
+  if (up == 2) {
+    if (delta == 0) fm_launch_one<2, 0, IN_F16>(a, ntiles, s);
+    else fm_launch_one<2, 1, IN_F16>(a, ntiles, s);
+  } else {
+    switch (delta) {
+      case 0: fm_launch_one<4, 0, IN_F16>(a, ntiles, s); break;
+      case 1: fm_launch_one<4, 1, IN_F16>(a, ntiles, s); break;
+      case 2: fm_launch_one<4, 2, IN_F16>(a, ntiles, s); break;
+      default: fm_launch_one<4, 3, IN_F16>(a, ntiles, s); break;
+    }
+  }
+}
+
+int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, int delta, int n, hipStream_t s) {
+  if (down != 2 || td != 12 || tu != 6 * up || (up != 2 && up != 4) || a.bias != nullptr || a.c_p % 16 != 0)
+    return IC2_E_UNSUPPORTED;
+  a.tiles_x = (int)ceil_div(a.out_w, 16);
+  a.tiles_y = (int)ceil_div(a.out_h, 16);
+  a.cblocks = a.c_p / 16;
+  const int64_t grid = (int64_t)n * a.tiles_y * a.tiles_x * a.cblocks;
+  if (grid >= (1LL << 31)) return IC2_E_UNSUPPORTED;
+  if (in_f16) fm_launch<true>(a, up, delta, (int)grid, s);
+  else fm_launch<false>(a, up, delta, (int)grid, s);
+  return IC2_OK;
+}
+
+}  // namespace ic2

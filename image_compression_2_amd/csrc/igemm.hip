@@ -97,6 +97,15 @@ __device__ __forceinline__ void ig_epilogue(const IgemmArgs& a, const f32x4 (&ac
           pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.y) + e) = pk;
+        } else if (a.out_dtype == IC2_F16) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          float s_[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s_[r] = __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
+          uint2 pk;
+          pk.x = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[0], (_Float16)s_[1]});
+          pk.y = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[2], (_Float16)s_[3]});
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.y) + e) = pk;
         } else {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + e) = make_float4(v[0], v[1], v[2], v[3]);
         }
@@ -531,7 +540,8 @@ extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, 
                               float clamp, float out_mul, int out_layout, void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
   IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_igemm: bad dtype %d", dtype);
-  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16, "conv_igemm: bad out dtype %d", out_dtype);
+  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout == IC2_LAYOUT_NHWC),
+                "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
                 "conv_igemm: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
   IC2_CHECK_ARG(n > 0 && h > 0 && w_ > 0 && kh > 0 && kw > 0 && pad >= 0, "conv_igemm: bad geometry");

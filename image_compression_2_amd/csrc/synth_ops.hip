@@ -73,41 +73,62 @@ __global__ void __launch_bounds__(256) upfirdn2d_kernel(const T* __restrict__ x,
 }
 
 // ------------------------------------------------------------------------------------------------
-// fully connected: one wave per output feature, lanes over the input features, 8 samples at a time
+// fully connected: a workgroup = FC_OPB output features x 32 sample rows; each row's dot products are
+// split over 8 lanes (contiguous K slices, float4 loads issued before the FMAs) and closed by
+// three xor-shuffles.  Latency-bound sizes (32 x 512 x 512) -> 256 workgroups, one load round trip.
 // ------------------------------------------------------------------------------------------------
+constexpr int FC_OPB = 2;
+
 __global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                  const float* __restrict__ b, float* __restrict__ y, int n, int in_f,
                                                  int out_f, float w_gain, float b_gain, int act, float alpha,
-                                                 float act_gain) {
-  const int lane = threadIdx.x & 63;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (o >= out_f) return;
-  const float* wr = w + (int64_t)o * in_f;
-  for (int n0 = 0; n0 < n; n0 += 8) {
-    float acc[8];
+                                                 float act_gain, int vec) {
+  const int t = threadIdx.x;
+  const int r = t >> 3, sl = t & 7;
+  const int nn = blockIdx.y * 32 + r;
+  const int o0 = blockIdx.x * FC_OPB;
+  const int len = (in_f + 7) >> 3;
+  const int i0 = sl * len, i1 = min(in_f, i0 + len);
+  const float* xr = x + (int64_t)(nn < n ? nn : 0) * ldx;
+  const float* wr[FC_OPB];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    for (int i = lane; i < in_f; i += 64) {
-      const float wv = wr[i];
+  for (int o = 0; o < FC_OPB; ++o) wr[o] = w + (int64_t)min(o0 + o, out_f - 1) * in_f;
+  float acc[FC_OPB];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (n0 + k < n) acc[k] += x[(int64_t)(n0 + k) * ldx + i] * wv;
+  for (int o = 0; o < FC_OPB; ++o) acc[o] = 0.f;
+  if (vec) {  // in_f % 32 == 0 and ldx % 4 == 0: every slice is whole float4s
+#pragma unroll 8
+    for (int i = i0; i < i1; i += 4) {
+      const float4 xv = *reinterpret_cast<const float4*>(xr + i);
+#pragma unroll
+      for (int o = 0; o < FC_OPB; ++o) {
+        const float4 wv = *reinterpret_cast<const float4*>(wr[o] + i);
+        acc[o] += xv.x * wv.x + xv.y * wv.y + xv.z * wv.z + xv.w * wv.w;
+      }
     }
+  } else {
+#pragma unroll 4
+    for (int i = i0; i < i1; ++i) {
+      const float xv = xr[i];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float v = acc[k];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      acc[k] = v;
+      for (int o = 0; o < FC_OPB; ++o) acc[o] += xv * wr[o][i];
     }
-    if (lane < 8 && n0 + lane < n) {
-      float v = 0.f;
+  }
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k == lane) v = acc[k];
-      v = v * w_gain + (b ? b[o] * b_gain : 0.f);
+  for (int o = 0; o < FC_OPB; ++o) {
+    float v = acc[o];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    acc[o] = v;
+  }
+  if (sl == 0 && nn < n) {
+#pragma unroll
+    for (int o = 0; o < FC_OPB; ++o) {
+      if (o0 + o >= out_f) break;
+      float v = acc[o] * w_gain + (b ? b[o0 + o] * b_gain : 0.f);
       if (act == IC2_ACT_LRELU) v = (v < 0.f ? v * alpha : v) * act_gain;
-      y[(int64_t)(n0 + lane) * out_f + o] = v;
+      y[(int64_t)nn * out_f + o0 + o] = v;
     }
   }
 }
@@ -161,26 +182,31 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // modulation / demodulation coefficients
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) style_norm_kernel(const float* __restrict__ s, int64_t total,
-                                                         float* __restrict__ out) {
-  __shared__ double red[256];
-  double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < total; i += 256) acc += (double)s[i] * (double)s[i];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+// xscale = s * g with g = rsqrt(mean(s^2)) over the whole batch (demod) or style_gain: one workgroup,
+// f64 sum of squares (fixed order: per-thread strided sums, wave xor-tree, then 16 wave totals in order)
+__global__ void __launch_bounds__(1024) style_xscale_kernel(const float* __restrict__ s, int n, int cin, int cin_p,
+                                                            int demod, float style_gain, float* __restrict__ xs) {
+  __shared__ double red[16];
+  __shared__ float gsh;
+  const int64_t total = (int64_t)n * cin;
+  float g = style_gain;
+  if (demod) {
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < total; i += 1024) acc += (double)s[i] * (double)s[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int k = 0; k < 16; ++k) t += red[k];
+      gsh = rsqrtf((float)(t / (double)total));
+    }
+    __syncthreads();
+    g = gsh;
   }
-  if (threadIdx.x == 0) out[0] = rsqrtf((float)(red[0] / (double)total));
-}
-
-__global__ void __launch_bounds__(256) xscale_kernel(const float* __restrict__ s, int n, int cin, int cin_p,
-                                                     const float* __restrict__ snorm, float style_gain,
-                                                     float* __restrict__ xs) {
-  const int64_t total = (int64_t)n * cin_p;
-  const float g = snorm ? snorm[0] : style_gain;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+  const int64_t tot_p = (int64_t)n * cin_p;
+  for (int64_t e = threadIdx.x; e < tot_p; e += 1024) {
     const int i = (int)(e % cin_p);
     const int64_t nn = e / cin_p;
     xs[e] = i < cin ? s[nn * cin + i] * g : 0.f;
@@ -332,8 +358,10 @@ extern "C" int ic2_upfirdn2d(const void* x, void* y, int dtype, int64_t nc, int 
 extern "C" int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y, int n, int in_f,
                       int out_f, float w_gain, float b_gain, int act, float alpha, float act_gain, void* stream) {
   IC2_CHECK_ARG(x && w && y && n > 0 && in_f > 0 && out_f > 0 && ldx >= in_f, "fc: bad arguments");
-  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)ceil_div(out_f, 4)), dim3(256), 0, as_stream(stream), x, ldx, w, b, y, n,
-                     in_f, out_f, w_gain, b_gain, act, alpha, act_gain);
+  const int vec = in_f % 32 == 0 && ldx % 4 == 0 && ((uintptr_t)x | (uintptr_t)w) % 16 == 0;
+  dim3 grid((unsigned)ceil_div(out_f, FC_OPB), (unsigned)ceil_div(n, 32));
+  hipLaunchKernelGGL(fc_kernel, grid, dim3(256), 0, as_stream(stream), x, ldx, w, b, y, n, in_f, out_f, w_gain, b_gain,
+                     act, alpha, act_gain, vec);
   IC2_CHECK_LAUNCH("fc");
   return IC2_OK;
 }
@@ -359,11 +387,11 @@ extern "C" int ic2_modconv_prep(const float* styles, const float* wsq, int n, in
                                 int demod, float style_gain, float input_gain, float* xscale_out, float* oscale_out,
                                 float* scratch, void* stream) {
   IC2_CHECK_ARG(styles && xscale_out && oscale_out && n > 0 && cin > 0 && cout > 0, "modconv_prep: bad arguments");
-  IC2_CHECK_ARG(!demod || (wsq && scratch), "modconv_prep: demodulation needs wsq and scratch");
+  IC2_CHECK_ARG(!demod || wsq, "modconv_prep: demodulation needs wsq");
   hipStream_t s = as_stream(stream);
-  if (demod) hipLaunchKernelGGL(style_norm_kernel, dim3(1), dim3(256), 0, s, styles, (int64_t)n * cin, scratch);
-  hipLaunchKernelGGL(xscale_kernel, dim3(grid_1d((int64_t)n * cin_p)), dim3(256), 0, s, styles, n, cin, cin_p,
-                     demod ? scratch : nullptr, style_gain, xscale_out);
+  (void)scratch;
+  hipLaunchKernelGGL(style_xscale_kernel, dim3(1), dim3(1024), 0, s, styles, n, cin, cin_p, demod, style_gain,
+                     xscale_out);
   hipLaunchKernelGGL(oscale_kernel, dim3((unsigned)ceil_div((int64_t)n * cout_p, 4)), dim3(256), 0, s, xscale_out, wsq,
                      n, cin, cin_p, cout, cout_p, demod, input_gain, oscale_out);
   IC2_CHECK_LAUNCH("modconv_prep");

@@ -18,7 +18,8 @@ def uint8_sse(a, b):
     assert a.shape == b.shape
     n = a.shape[0]
     out = torch.empty(n, dtype=torch.float64, device=a.device)
-    nv.call("ic2_uint8_sse", nv.ptr(a), nv.ptr(b), n, a[0].numel(), nv.ptr(out), nv.stream_of(a))
+    scratch = torch.empty(int(nv.query("ic2_uint8_sse_scratch_doubles", n)), dtype=torch.float64, device=a.device)
+    nv.call("ic2_uint8_sse", nv.ptr(a), nv.ptr(b), n, a[0].numel(), nv.ptr(out), nv.ptr(scratch), nv.stream_of(a))
     return out
 
 

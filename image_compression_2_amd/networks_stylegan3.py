@@ -12,7 +12,8 @@ seeded parameter construction order, and a forward that runs entirely in libic2o
                 y = oscale * conv(W_norm, x) + bias   ic2_conv_igemm   (MFMA, NHWC)
                 x = filtered_lrelu(y) * xscale_next   ic2_flrelu_nhwc  (fused FIR, NHWC)
 
-``precision='bf16'`` stores activations and weights in bf16 (fp32 accumulate, fp32 FIR math);
+``precision='bf16'`` stores activations and weights in bf16 (fp32 accumulate; the conv output that feeds
+the filtered lrelu is f16, whose FIR runs on MFMA with f16 operands and fp32 accumulation);
 ``precision='fp32'`` (default) is the parity mode (exact-fp32 MFMA).
 """
 from __future__ import annotations
@@ -293,8 +294,10 @@ class SynthesisLayer(torch.nn.Module):
                     self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp),
                     nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW, stream)
             return out
-        y = torch.empty([n, conv, conv, self.cout_p], dtype=dt, device=x.device)
-        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(dt), n, s_in, s_in,
+        # bf16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16
+        ydt = torch.float16 if dt == torch.bfloat16 else dt
+        y = torch.empty([n, conv, conv, self.cout_p], dtype=ydt, device=x.device)
+        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
                 self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0, 0.0,
                 1.0, -1.0, 1.0, nv.NHWC, stream)
         s_out = int(self.out_size[0])
@@ -303,7 +306,7 @@ class SynthesisLayer(torch.nn.Module):
         fd = self._fd
         px0, px1, py0, py1 = self.padding
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
-        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, self.cout_p, conv,
+        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(ydt), nv.dtype_code(dt), n, self.cout_p, conv,
                 conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
                 1 if fu is None else fu.shape[0], None if fd is None else fd.ctypes.data_as(ctypes.c_void_p),
                 1 if fd is None else fd.shape[0], None, self.up_factor, self.down_factor, px0, px1, py0, py1,

@@ -7,7 +7,7 @@
  *     nothing is allocated, freed or synchronised inside -> every call is hipGraph-capturable;
  *   - work is enqueued on `stream` (a hipStream_t passed as void*; NULL = the legacy default stream);
  *   - return IC2_OK (0) or an IC2_E_* code; ic2_last_error() returns the thread-local message;
- *   - dtype codes: IC2_F32 = 0, IC2_BF16 = 1.  Activations on the synthesis path are NHWC with a
+ *   - dtype codes: IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 (f16 only where an entry point says so).  Activations on the synthesis path are NHWC with a
  *     channel stride padded to a multiple of 32 ("c_p"); padded channels hold zeros.
  *
  * The reference has no native code and no C ABI: each entry point names the Python
@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
-enum { IC2_F32 = 0, IC2_BF16 = 1 };
+enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 };
 enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
 enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1 };
 
@@ -89,7 +89,9 @@ int ic2_filtered_lrelu(const void* x, void* y, int dtype, int64_t n, int64_t c, 
 
 /* The synthesis-path variant of the same fused op: NHWC in/out with padded channel stride c_p,
  * bias already folded into the producer (b may be NULL), and an optional per-(sample, channel)
- * post_scale [n][c_p] (the NEXT layer's modulation, see ic2_modconv_prep) applied to the output. */
+ * post_scale [n][c_p] (the NEXT layer's modulation, see ic2_modconv_prep) applied to the output.
+ * bf16 -> bf16 and the SG3-T configurations (up 2/4 with 6*up taps, down 2 with 12) run on MFMA with f16
+ * operands; dtype_in may then also be IC2_F16 (the conv epilogue's f16 output). */
 int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_out, int n, int c_p, int in_h, int in_w,
                     int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps, const float* b,
                     int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
@@ -113,7 +115,7 @@ int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_
  *   demod:  s' = s * rsqrt(mean(s^2)) (batch-global), xscale = s',
  *           oscale = input_gain * rsqrt(sum_i s'^2 * wsq[o][i] + 1e-8);
  *   !demod: xscale = s * style_gain, oscale = input_gain.
- * styles [n][cin] f32; xscale_out [n][cin_p]; oscale_out [n][cout_p]; scratch: 1 float. */
+ * styles [n][cin] f32; xscale_out [n][cin_p]; oscale_out [n][cout_p]; scratch: unused (may be NULL). */
 int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int cout, int cin_p, int cout_p,
                      int demod, float style_gain, float input_gain, float* xscale_out, float* oscale_out,
                      float* scratch, void* stream);
@@ -174,8 +176,11 @@ int ic2_reparameterize(const float* params, const float* eps, int n, int num_ws,
 /* ------------------------------------------------------------------------------ metrics ---- */
 
 /* PSNR support (hvae_training.py:368-388 uint8 conversion): per image sum of squared differences of
- * trunc(clamp(v*0.5+0.5,0,1)*255) between two NCHW f32 batches -> sse_out [n_img] (f64). */
-int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img, double* sse_out, void* stream);
+ * trunc(clamp(v*0.5+0.5,0,1)*255) between two NCHW f32 batches -> sse_out [n_img] (f64).
+ * scratch: ic2_uint8_sse_scratch_doubles(n_img) doubles (per-chunk partials; deterministic). */
+int64_t ic2_uint8_sse_scratch_doubles(int64_t n_img);
+int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img, double* sse_out, double* scratch,
+                  void* stream);
 
 /* F.interpolate(mode='bilinear', align_corners=False, no antialias) of StyleGAN3Compressor.forward
  * (stylegan3_hvae_full.py:277-279), NCHW f32. */

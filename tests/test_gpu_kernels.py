@@ -166,6 +166,48 @@ def test_filtered_lrelu_nchw(cuda, case, dtype):
     assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
 
 
+# ------------------------------------------------------------------ fused FLR, synthesis (NHWC) path
+@pytest.fixture(scope="module")
+def gen256_bf16_layers():
+    torch.manual_seed(1)
+    return ic2.Generator(img_resolution=256).synthesis.layers()
+
+
+@pytest.mark.parametrize("layer", [0, 3, 5, 10, 13])
+@pytest.mark.parametrize("c_p", [32, 64])
+@pytest.mark.parametrize("in_dtype", [torch.bfloat16, torch.float16])
+def test_flrelu_nhwc_bf16_matches_oracle(cuda, gen256_bf16_layers, layer, c_p, in_dtype):
+    """The NHWC filtered-lrelu with bf16 output (MFMA formulation, f16 operands) on SG3-T-256 layer
+    geometries (up 2 / up 4, positive and negative padding), bf16 or f16 input, with a post_scale,
+    against the fp64 reference composition."""
+    import ctypes
+    L = gen256_bf16_layers[layer]
+    n = 2
+    conv = int(L.in_size[0]) + 2
+    s_out = int(L.out_size[0])
+    g = torch.Generator().manual_seed(20 + layer)
+    x = (torch.randn(n, c_p, conv, conv, generator=g) * 2).to(in_dtype).float()
+    x[:, :, :3, :5] = 300.0  # exercises the clamp
+    ps = torch.rand(n, c_p, generator=g) + 0.5
+    xd = x.permute(0, 2, 3, 1).contiguous().to(cuda, in_dtype)
+    out = torch.empty(n, s_out, s_out, c_p, device=cuda, dtype=torch.bfloat16)
+    psd = ps.to(cuda)
+    nv.call("ic2_flrelu_nhwc", nv.ptr(xd), nv.ptr(out), nv.dtype_code(in_dtype), nv.BF16, n, c_p, conv, conv, s_out,
+            s_out, L._fu.ctypes.data_as(ctypes.c_void_p), L._fu.shape[0], L._fd.ctypes.data_as(ctypes.c_void_p),
+            L._fd.shape[0], None, L.up_factor, L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0,
+            nv.ptr(psd), nv.stream_of(xd))
+    torch.cuda.synchronize()
+    r = sg3.filtered_lrelu(x.double(), torch.from_numpy(L._fu).double(), torch.from_numpy(L._fd).double(), None,
+                           up=L.up_factor, down=L.down_factor, padding=L.padding, gain=np.sqrt(2), slope=0.2,
+                           clamp=256.0) * ps.double()[:, :, None, None]
+    y = out.float().cpu().permute(0, 3, 1, 2)
+    assert y.shape == r.shape
+    err = (y.double() - r).abs()
+    scale = r.abs().max().item()
+    assert err.max().item() < 2e-2 * (1 + scale), (err.max().item(), scale)
+    assert err.mean().item() < 2e-3 * (1 + r.abs().mean().item())
+
+
 # ------------------------------------------------------------------ implicit-GEMM conv (MFMA)
 IGEMM_CASES = [(3, 32, 19, 1, 0), (64, 96, 12, 1, 0), (181, 128, 9, 2, 0), (512, 512, 6, 2, 0),
                (256, 362, 10, 2, 1), (96, 64, 13, 1, 2), (128, 181, 11, 2, 3), (512, 256, 7, 2, 4),
@@ -206,11 +248,55 @@ def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16):
     assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
 
 
+# ------------------------------------------------------------------ fully connected (fp32 reference)
+@pytest.mark.parametrize("n,in_f,out_f,ldx,act", [(32, 512, 512, 512, 0), (40, 512, 7, 8192, 0), (3, 100, 33, 100, 1),
+                                                  (5, 128, 256, 128, 1)])
+def test_fc_matches_torch(cuda, n, in_f, out_f, ldx, act):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, ldx, generator=g)
+    w = torch.randn(out_f, in_f, generator=g)
+    b = torch.randn(out_f, generator=g)
+    y = torch.empty(n, out_f, device=cuda)
+    wg, bg = 1 / np.sqrt(in_f), 0.5
+    xd, wd, bd = x.to(cuda), w.to(cuda), b.to(cuda)  # keep the device copies alive across the call
+    nv.call("ic2_fc", nv.ptr(xd), ldx, nv.ptr(wd), nv.ptr(bd), nv.ptr(y), n, in_f, out_f,
+            float(wg), bg, act, 0.2, float(np.sqrt(2)) if act else 1.0, nv.stream_of(y))
+    torch.cuda.synchronize()
+    r = (x[:, :in_f].double() @ w.double().t()) * wg + b.double() * bg
+    if act:
+        r = F.leaky_relu(r, 0.2) * np.sqrt(2)
+    assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item())
+
+
+# ------------------------------------------------------------------ GroupNorm + lrelu (+ pool), fp32 reference
+@pytest.mark.parametrize("n,c,groups,h,w,pool", [(2, 64, 32, 5, 7, True), (3, 96, 32, 9, 6, False),
+                                                 (32, 512, 32, 2, 2, True), (1, 32, 32, 40, 33, True)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_norm_lrelu_pool_matches_torch(cuda, n, c, groups, h, w, pool, dtype):
+    from image_compression_2_amd.stylegan3_hvae_full import _group_norm_lrelu
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(n, c, h, w, generator=g) * 3 + 0.5
+    norm = torch.nn.GroupNorm(groups, c)
+    with torch.no_grad():
+        norm.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        norm.bias.copy_(torch.randn(c, generator=g))
+    r = F.leaky_relu(norm(x), 0.2)
+    if pool:
+        r = F.avg_pool2d(r, 2)
+    stream = nv.stream_of()
+    xin = _to_nhwc(x.to(cuda), dtype, stream)
+    out = _group_norm_lrelu(norm.to(cuda), xin, pool, dtype, stream)
+    y = _to_nchw(out, stream)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
+
+
 # ------------------------------------------------------------------ metric / resize
-def test_uint8_sse_matches_reference_definition(cuda):
+@pytest.mark.parametrize("shape", [(3, 3, 16, 16), (2, 3, 7, 5), (1, 3, 256, 256)])
+def test_uint8_sse_matches_reference_definition(cuda, shape):
     g = torch.Generator().manual_seed(4)
-    a = torch.rand(3, 3, 16, 16, generator=g) * 2.4 - 1.2
-    b = torch.rand(3, 3, 16, 16, generator=g) * 2 - 1
+    a = torch.rand(*shape, generator=g) * 2.4 - 1.2
+    b = torch.rand(*shape, generator=g) * 2 - 1
     sse = icm.uint8_sse(a.to(cuda), b.to(cuda)).cpu().numpy()
     assert np.array_equal(sse, om.sse_uint8(a, b))
     assert icm.psnr(a.to(cuda), b.to(cuda)) == pytest.approx(om.psnr(a, b), abs=1e-9)
