@@ -46,9 +46,9 @@ def parse():
 
 
 class IgemmTimer:
-    """Wraps every ic2_conv_igemm launch (the dominant kernel: all encoder convs, the synthesis input
-    1x1 and every modulated conv) with HIP events on the launching stream -- torch's current stream,
-    which is the stream every libic2ops kernel is enqueued on."""
+    """Wraps every ic2_conv_igemm[_ws] call (the dominant kernel, plus its split-K combine where the launch
+    plan splits K: all encoder convs, the synthesis input 1x1 and every modulated conv) with HIP events on
+    the launching stream -- torch's current stream, which is the stream every libic2ops kernel is enqueued on."""
 
     def __init__(self, nv):
         self.nv = nv
@@ -60,7 +60,7 @@ class IgemmTimer:
         timer = self
 
         def call(name, *args):
-            if not timer.enabled or name != "ic2_conv_igemm":
+            if not timer.enabled or name not in ("ic2_conv_igemm", "ic2_conv_igemm_ws"):
                 return timer.orig(name, *args)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()

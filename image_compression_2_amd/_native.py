@@ -42,6 +42,9 @@ _SIGS = {
     "ic2_modconv_prep": [_P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P],
     "ic2_conv_igemm": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I,
                        _P],
+    "ic2_conv_igemm_ws_bytes": [_I, _I, _I, _I, _I, _I, _I, _I, _I],
+    "ic2_conv_igemm_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F,
+                          _I, _P, _I64, _P],
     "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "ic2_nhwc_to_nchw": [_P, _I, _P, _I, _I, _I, _I, _I, _P],
@@ -55,7 +58,7 @@ _SIGS = {
     "ic2_uint8_sse": [_P, _P, _I64, _I64, _P, _P, _P],
     "ic2_resize_bilinear": [_P, _P, _I64, _I, _I, _I, _I, _P],
 }
-_RESTYPE = {"ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
+_RESTYPE = {"ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
             "ic2_uint8_sse_scratch_doubles": _I64}
 
 _lib = None
@@ -104,6 +107,16 @@ def call(name, *args):
 
 def query(name, *args):
     return getattr(load(), name)(*args)
+
+
+def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo, oscale, bias,
+               act, slope, act_gain, clamp, out_mul, out_layout, stream, device):
+    """ic2_conv_igemm with the split-K workspace the launch plan asks for (a stream-ordered torch
+    allocation, so the call stays capturable in a hipGraph)."""
+    nbytes = int(query("ic2_conv_igemm_ws_bytes", dtype, n, h, w_, cin_p, cout_p, kh, kw, pad))
+    ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=device) if nbytes > 0 else None
+    return call("ic2_conv_igemm_ws", x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho,
+                wo, oscale, bias, act, slope, act_gain, clamp, out_mul, out_layout, ptr(ws), nbytes, stream)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -18,6 +18,9 @@
 // reads apply the same XOR (conflict-free for bf16, 2-way for f32).  Out-of-image taps and padded
 // output channels read a zero line instead of branching.  Blocks are remapped so consecutive
 // logical tiles (which share input rows / weight panels) land on the same XCD's L2.
+// Launches that would not fill the chip (the encoder's 16^2 .. 2^2 blocks) split K over gridDim.y:
+// each slice stores f32 partial sums in a caller-owned workspace and igemm_splitk_reduce_kernel
+// combines them in slice order (deterministic) through the same epilogue.
 #include "common.h"
 
 #include <cstdlib>
@@ -33,10 +36,11 @@ struct IgemmArgs {
   void* y;
   const float* oscale;
   const float* bias;
+  float* ws;    // split-K partial sums [gridDim.y][M][cout_p] f32 (gridDim.y > 1 only)
   int n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo;
   int M;        // n * ho * wo
   int K;        // kh * kw * cin_p
-  int nq;       // K / 32
+  int nq;       // K-chunks: K / 32 (K / 64 for the 8-phase kernels)
   int tiles_o;  // ceil(cout_p / BO)
   int nblocks;  // tiles_o * tiles_p
   int group;    // p-tiles per o-sweep (tile_coords)
@@ -62,13 +66,55 @@ struct IgCfg {
   __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
 };
 
-// Epilogue shared by both kernels: lane holds C[o = obase + 16i + 4*fh + r][p = pbase + 16j + fr].
-// y = act(acc * oscale[n][o] + bias[o]) * out_mul, stored NHWC (bf16/f32) or NCHW (f32, o < cout_valid).
+// y = act(acc * oscale[n][o] + bias[o]) * out_mul for the channels ob .. ob+3 of output pixel p = (nn, pix),
+// stored NHWC (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only).
+__device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4]) {
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), bi = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.oscale) sc = *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob);
+  if (a.bias) bi = *reinterpret_cast<const float4*>(a.bias + ob);
+  const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, biv[4] = {bi.x, bi.y, bi.z, bi.w};
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = acc[r] * scv[r] + biv[r];
+    if (a.act) t = lrelu_gain_clamp(t, a.slope, a.act_gain, a.clamp);
+    v[r] = t * a.out_mul;
+  }
+  if (a.out_layout == IC2_LAYOUT_NHWC) {
+    const int64_t e = (int64_t)p * a.cout_p + ob;
+    if (a.out_dtype == IC2_BF16) {
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.y) + e) = pk;
+    } else if (a.out_dtype == IC2_F16) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      float s_[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_[r] = __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
+      uint2 pk;
+      pk.x = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[0], (_Float16)s_[1]});
+      pk.y = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[2], (_Float16)s_[3]});
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.y) + e) = pk;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + e) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    float* yo = reinterpret_cast<float*>(a.y);
+    const int hw = a.ho * a.wo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (ob + r < a.cout_valid) yo[((int64_t)nn * a.cout_valid + ob + r) * hw + pix] = v[r];
+  }
+}
+
+// Epilogue shared by the kernels: lane holds C[o = obase + 16i + 4*fh + r][p = pbase + 16j + fr].
+// A split-K slice (gridDim.y > 1) stores its raw partial sums instead.
 template <int I, int J>
 __device__ __forceinline__ void ig_epilogue(const IgemmArgs& a, const f32x4 (&acc)[I][J], int obase, int pbase, int fr,
                                             int fh) {
   const int hw = a.ho * a.wo;
-  const bool has_os = a.oscale != nullptr, has_b = a.bias != nullptr;
+  const bool partial = gridDim.y > 1;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int p = pbase + j * 16 + fr;
@@ -79,42 +125,12 @@ __device__ __forceinline__ void ig_epilogue(const IgemmArgs& a, const f32x4 (&ac
     for (int i = 0; i < I; ++i) {
       const int ob = obase + i * 16 + 4 * fh;
       if (ob >= a.cout_p) continue;
-      float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), bi = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (has_os) sc = *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob);
-      if (has_b) bi = *reinterpret_cast<const float4*>(a.bias + ob);
-      float v[4];
-      const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, biv[4] = {bi.x, bi.y, bi.z, bi.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[i][j][r] * scv[r] + biv[r];
-        if (a.act) t = lrelu_gain_clamp(t, a.slope, a.act_gain, a.clamp);
-        v[r] = t * a.out_mul;
+      if (partial) {
+        *reinterpret_cast<f32x4*>(a.ws + ((int64_t)blockIdx.y * a.M + p) * a.cout_p + ob) = acc[i][j];
+        continue;
       }
-      if (a.out_layout == IC2_LAYOUT_NHWC) {
-        const int64_t e = (int64_t)p * a.cout_p + ob;
-        if (a.out_dtype == IC2_BF16) {
-          uint2 pk;
-          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.y) + e) = pk;
-        } else if (a.out_dtype == IC2_F16) {
-          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-          float s_[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s_[r] = __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
-          uint2 pk;
-          pk.x = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[0], (_Float16)s_[1]});
-          pk.y = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[2], (_Float16)s_[3]});
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.y) + e) = pk;
-        } else {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + e) = make_float4(v[0], v[1], v[2], v[3]);
-        }
-      } else {
-        float* yo = reinterpret_cast<float*>(a.y);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (ob + r < a.cout_valid) yo[((int64_t)nn * a.cout_valid + ob + r) * hw + pix] = v[r];
-      }
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      ig_store4(a, p, nn, pix, ob, v);
     }
   }
 }
@@ -203,8 +219,11 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
     w_base[k] = o < a.cout_p ? wg + (int64_t)o * a.K * ESZ + chl * 16 : nullptr;
   }
   const int CB = a.cin_p >> 5;
+  // split-K: slice blockIdx.y of gridDim.y covers the K-chunks [q0, q1)
+  const int q0 = (int)((int64_t)a.nq * blockIdx.y / gridDim.y);
+  const int q1 = (int)((int64_t)a.nq * (blockIdx.y + 1) / gridDim.y);
   // chunk cursor of the next DMA (uniform): chunk index, its tap (ky, kx) and 32-channel block
-  int iq = 0, icb = 0, ikx = 0, iky = 0;
+  int iq = q0, icb = q0 % CB, ikx = (q0 / CB) % a.kw, iky = (q0 / CB) / a.kw;
   const int64_t xrow = (int64_t)a.w_ * a.cin_p * ESZ;
 
 #define IC2_IG_ISSUE(buf_)                                                                                    \
@@ -224,8 +243,8 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)xs,                     \
                                        (__attribute__((address_space(3))) void*)(xl_ + x_seg[k]), 16, 0, 0); \
     }                                                                                                        \
-    { /* advance (branch-free); past the end the last chunk is re-issued (never consumed) */               \
-      const int adv = iq + 1 < a.nq;                                                                         \
+    { /* advance (branch-free); past the slice end the last chunk is re-issued (never consumed) */         \
+      const int adv = iq + 1 < q1;                                                                           \
       iq += adv;                                                                                             \
       icb += adv;                                                                                            \
       const int wrap = icb == CB;                                                                            \
@@ -249,7 +268,7 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
   const int fr = lane & 15;
   const int fh = lane >> 4;
 
-  for (int q = 0; q < a.nq; ++q) {
+  for (int q = 0; q < q1 - q0; ++q) {
     const int cur = q % NSTAGE;
     if constexpr (NSTAGE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * C::PER) : "memory");
@@ -310,39 +329,72 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
   ig_epilogue<I, J>(a, acc, o0 + wo_ * C::TO, m0 + wp_ * C::TP, fr, fh);
 }
 
+// split-K combine: sum the slices in slice order (deterministic), then the epilogue; one thread per
+// (pixel, 4 channels)
+__global__ void __launch_bounds__(256) igemm_splitk_reduce_kernel(IgemmArgs a, int splits) {
+  const int c4 = a.cout_p >> 2;
+  const int total = a.M * c4;  // < 2^31 (checked by the launcher)
+  const int hw = a.ho * a.wo;
+  const int64_t slice = (int64_t)a.M * a.cout_p;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int p = e / c4;
+    const int ob = (e - p * c4) * 4;
+    const float* src = a.ws + (int64_t)p * a.cout_p + ob;
+    f32x4 s = *reinterpret_cast<const f32x4*>(src);
+    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(src + k * slice);
+    const int nn = p / hw;
+    const float v[4] = {s[0], s[1], s[2], s[3]};
+    ig_store4(a, p, nn, p - nn * hw, ob, v);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
-// 256 x 256 bf16 tile, 64-deep K-tiles (64 channels of one tap), 8 waves = 2 o-groups x 4 p-groups,
-// each wave owning 128 x 64 outputs.  Eight phases per iteration (two K-tiles, LDS double buffer):
-// phase = (ds_read the quadrant's fragments, DMA one half-tile, [counted vmcnt], s_barrier,
-// 16 MFMAs at raised priority, s_barrier).  The o-group 1 waves run one barrier behind group 0, so on
-// every SIMD (one wave of each group) one wave's MFMAs overlap the other's LDS reads and DMA issue.
+// 8-phase kernels, 64-deep K-tiles (64 channels of one tap), 8 waves each owning 128 x 64 outputs:
+//   OG = 2: 256 x 256 tile, 2 o-groups x 4 p-groups;
+//   OG = 1: 128 x 512 tile (the cout_p <= 128 layers), 1 o-group x 8 p-groups.
+// Eight phases per iteration (two K-tiles, LDS double buffer): phase = (ds_read the quadrant's
+// fragments, DMA one half-tile, [counted vmcnt], s_barrier, 16 MFMAs at raised priority, s_barrier).
+// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD (one wave of each half) one wave's
+// MFMAs overlap the other's LDS reads and DMA issue.
 //   quadrant per phase&3 : (qm,qn) = (0,0) (0,1) (1,1) (1,0); reads A(qm)+B(qn), B(1), A(1), B(0)
 //   half-tile restaged   : ph0 buf1.A1<-t+1  ph1 buf1.B0<-t+1  ph2..5 buf0.{A0,B1,A1,B0}<-t+2
 //                          ph6 buf1.A0<-t+3  ph7 buf1.B1<-t+3      (t = 2*iteration)
 // Every half is restaged >= 2 phases after its last read (WAR) and read >= 1 phase after the
-// vmcnt(4) + barrier that retires it (RAW: waits in phases 3 and 7).  Half-tile qm of A = the rows
-// {128*g + 64*qm + [0, 64)}; half-tile qn of B = the rows {64*g + 32*qn + [0, 32)}: 16 KiB, two
-// 1-KiB DMA instructions per wave.  LDS rows are 128 B, 16-B chunk c stored at c ^ ((row >> 1) & 7)
-// (conflict-free ds_read_b128 for the fragment lane groups).
-constexpr int G8_BUF = 65536, G8_BOFF = 32768;  // bytes: one K-tile buffer, B offset in it
+// vmcnt + barrier that retires it (RAW: the waits in phases 3 and 7 leave only the two newest halves,
+// NA + NB DMA instructions, in flight).  Half-tile qm of A = the rows {128*og + 64*qm + [0, 64)};
+// half-tile qn of B = the rows {64*pg + 32*qn + [0, 32)}: NA = OG and NB = 4 / OG 1-KiB DMA
+// instructions per wave.  LDS rows are 128 B, 16-B chunk c stored at c ^ ((row >> 1) & 7)
+// (conflict-free ds_read_b128 for the fragment lane groups).  64-row quadrants lying wholly in the
+// o-padding (cout_p 64 / 192 / 384) skip their MFMAs: their accumulators stay 0, which is what those
+// rows hold, and the SIMD's partner wave gets the matrix pipe to itself.
+template <int OG>
+struct G8 {
+  static constexpr int BO = 128 * OG, BP = 512 / OG;
+  static constexpr int NA = OG, NB = 4 / OG;                    // DMA instructions per wave per half-tile
+  static constexpr int BOFF = BO * 128, BUF = (BO + BP) * 128;  // bytes: B offset in a buffer, one buffer
+};
 constexpr uint32_t kOob = 0x7ffffff0u;            // num_records of a live descriptor = the zero-answer offset
 constexpr int kRsrcWord3 = 0x00020000;            // raw buffer descriptor word 3 (gfx9 family)
 __device__ __forceinline__ int g8_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 __device__ __forceinline__ int g8_arow(int qm, int g, int l) { return (g >> 3) * 128 + qm * 64 + (g & 7) * 8 + l; }
 __device__ __forceinline__ int g8_brow(int qn, int g, int l) { return (g >> 2) * 64 + qn * 32 + (g & 3) * 8 + l; }
 
-__global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * G8_BUF];
+template <int OG>
+__device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
+  using G = G8<OG>;
+  constexpr int NA = G::NA, NB = G::NB;
+  __shared__ __attribute__((aligned(16))) char lds[2 * G::BUF];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid_u = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid_u >> 2;  // o-group (= ping-pong group)
-  const int wp_ = wid_u & 3;
+  const int half = wid_u >> 2;                     // waves 4-7 run one barrier behind waves 0-3
+  const int grp = OG == 2 ? half : 0;              // o-group
+  const int wp_ = OG == 2 ? (wid_u & 3) : wid_u;   // p-group (64 pixels)
   const int logical = xcd_remap(blockIdx.x, a.nblocks);
   int o_tile, p_tile;
   tile_coords(logical, a.tiles_o, a.nblocks / a.tiles_o, a.group, o_tile, p_tile);
-  const int o0 = o_tile * 256;
-  const int m0 = p_tile * 256;
+  const int o0 = o_tile * G::BO;
+  const int m0 = p_tile * G::BP;
   const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
   const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
 
@@ -350,19 +402,21 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
   // Buffer loads (raw, stride 0): the per-K-tile part of the address is a scalar descriptor base, the
   // per-lane part a constant 32-bit offset; a tap outside the image / a row past M or cout_p gets the
   // offset kOob (>= num_records), which the hardware answers with zeros.  No per-lane 64-bit math.
-  uint32_t w_off[2][2], x_off[2][2], x_tap[2][2];
+  uint32_t w_off[2][NA], x_off[2][NB], x_tap[2][NB];
   const int hw = a.ho * a.wo;
   const int lrow = lane >> 3;                    // row within the 8-row block
   const int pch = lane & 7;                      // physical 16-B chunk written by this lane
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int g = wid_u + 8 * k;
-      const int ar = g8_arow(h, g, lrow);
+    for (int k = 0; k < NA; ++k) {
+      const int ar = g8_arow(h, wid_u + 8 * k, lrow);
       const int o = o0 + ar;
       w_off[h][k] = o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((ar >> 1) & 7)) << 4)) : kOob;
-      const int br = g8_brow(h, g, lrow);
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int br = g8_brow(h, wid_u + 8 * k, lrow);
       const int m = m0 + br;
       const bool ok = m < a.M;
       const int mm = ok ? m : 0;
@@ -380,6 +434,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
         }
       x_tap[h][k] = mask;
     }
+  }
   const int CB = a.cin_p >> 6;
 
   // K-tile cursor (uniform): tile index, tap (ky, kx), 64-channel block
@@ -402,8 +457,8 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
   {                                                                                                          \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(                                     \
         (void*)(wg + (int64_t)(c_).t * 128), 0, (c_).t < a.nq ? kOob : 0, kRsrcWord3);                        \
-    _Pragma("unroll") for (int k = 0; k < 2; ++k)                                                            \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G8_BUF + \
+    _Pragma("unroll") for (int k = 0; k < NA; ++k)                                                           \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G::BUF + \
                                                                                        g8_arow(h_, wid_u + 8 * k, 0) * 128), \
                                                16, w_off[h_][k], 0, 0, 0);                                   \
   }
@@ -413,10 +468,10 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
     const int64_t sh = ((int64_t)((c_).ky - a.pad) * a.w_ + ((c_).kx - a.pad)) * a.cin_p * 2 + (c_).cb * 128;  \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(xg + sh), 0,                  \
                                                                         (c_).t < a.nq ? kOob : 0, kRsrcWord3); \
-    _Pragma("unroll") for (int k = 0; k < 2; ++k) {                                                          \
+    _Pragma("unroll") for (int k = 0; k < NB; ++k) {                                                         \
       const uint32_t vo = ((x_tap[h_][k] >> tap) & 1u) ? x_off[h_][k] : kOob;                                \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G8_BUF + \
-                                                                                       G8_BOFF + g8_brow(h_, wid_u + 8 * k, 0) * 128), \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G::BUF + \
+                                                                                       G::BOFF + g8_brow(h_, wid_u + 8 * k, 0) * 128), \
                                                16, vo, 0, 0, 0);                                             \
     }                                                                                                        \
   }
@@ -430,6 +485,8 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
   const int fr = lane & 15;
   const int fh = lane >> 4;
   bf16x8 af[4][2], bfr[2][2];
+  const int orow = o0 + grp * 128;
+  const bool live0 = orow < a.cout_p, live1 = orow + 64 < a.cout_p;
 
   // prologue: tile 0 -> buf0 (all four halves), tile 1 -> buf1.A0 / buf1.B1 (what phases 6-7 would issue)
   Cur c0{0, 0, 0, 0};
@@ -440,17 +497,17 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
   IC2_G8_ISSUE_B(1, 0, c0);
   IC2_G8_ISSUE_A(0, 1, c1);
   IC2_G8_ISSUE_B(1, 1, c1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");
   __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();  // o-group 1 runs one barrier behind
+  if (half == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 run one barrier behind
   __builtin_amdgcn_sched_barrier(0);
 
 #define IC2_G8_READ_A(buf_, qm_)                                                                              \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int s = 0; s < 2; ++s) af[i][s] =    \
-      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G8_BUF + g8_off(grp * 128 + (qm_) * 64 + i * 16 + fr, 4 * s + fh));
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + g8_off(grp * 128 + (qm_) * 64 + i * 16 + fr, 4 * s + fh));
 #define IC2_G8_READ_B(buf_, qn_)                                                                              \
   _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int s = 0; s < 2; ++s) bfr[j][s] =   \
-      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G8_BUF + G8_BOFF +                                      \
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + G::BOFF +                                      \
                                        g8_off(wp_ * 64 + (qn_) * 32 + j * 16 + fr, 4 * s + fh));
 #define IC2_G8_COMPUTE(qm_, qn_, WAIT_)                                                                       \
   __builtin_amdgcn_sched_barrier(0);                                                                         \
@@ -459,15 +516,17 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                         \
   __builtin_amdgcn_sched_barrier(0);                                                                         \
   __builtin_amdgcn_s_setprio(1);                                                                             \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)               \
-      _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + i][(qn_) * 2 + j] =                      \
-          __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[(qm_) * 4 + i][(qn_) * 2 + j], 0, 0, 0); \
+  if ((qm_) == 0 ? live0 : live1) {                                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)             \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + i][(qn_) * 2 + j] =                    \
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[(qm_) * 4 + i][(qn_) * 2 + j], 0, 0, 0); \
+  }                                                                                                          \
   __builtin_amdgcn_s_setprio(0);                                                                             \
   __builtin_amdgcn_sched_barrier(0);                                                                         \
   __builtin_amdgcn_s_barrier();                                                                              \
   __builtin_amdgcn_sched_barrier(0);
 #define IC2_G8_NOWAIT (void)0
-#define IC2_G8_WAIT4 asm volatile("s_waitcnt vmcnt(4)" ::: "memory")
+#define IC2_G8_WAIT asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory")
 
   const int niter = (a.nq + 1) >> 1;
   Cur cn = c1;  // tile 2i+1
@@ -491,7 +550,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
     // phase 3: (1,0); buf0.B1 <- 2i+2; retire tile 2i+1 (buf1) for phases 4-7
     IC2_G8_READ_B(0, 0);
     IC2_G8_ISSUE_B(1, 0, cB);
-    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT4);
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
     // phase 4: buf1 quadrant (0,0); buf0.A1 <- 2i+2
     IC2_G8_READ_B(1, 0);
     IC2_G8_READ_A(1, 0);
@@ -508,36 +567,120 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmArgs a) {
     // phase 7: (1,0); buf1.B1 <- 2i+3; retire tile 2i+2 (buf0) for the next iteration
     IC2_G8_READ_B(1, 0);
     IC2_G8_ISSUE_B(1, 1, cC);
-    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT4);
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
     cn = cC;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail DMAs (zero tiles) before exit
-  if (grp == 0) __builtin_amdgcn_s_barrier();       // balance the o-group-1 offset barrier
+  if (half == 0) __builtin_amdgcn_s_barrier();      // balance the waves 4-7 offset barrier
 #undef IC2_G8_ISSUE_A
 #undef IC2_G8_ISSUE_B
 #undef IC2_G8_READ_A
 #undef IC2_G8_READ_B
 #undef IC2_G8_COMPUTE
 #undef IC2_G8_NOWAIT
-#undef IC2_G8_WAIT4
-  ig_epilogue<8, 4>(a, acc, o0 + grp * 128, m0 + wp_ * 64, fr, fh);
+#undef IC2_G8_WAIT
+  ig_epilogue<8, 4>(a, acc, orow, m0 + wp_ * 64, fr, fh);
 }
 
+// one non-template kernel per instance (a __global__ template's host stub is not emitted here)
+__global__ void __launch_bounds__(512, 1) igemm8_og2_kernel(IgemmArgs a) { igemm8_body<2>(a); }
+__global__ void __launch_bounds__(512, 1) igemm8_og1_kernel(IgemmArgs a) { igemm8_body<1>(a); }
+
 template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
-static void launch_igemm(IgemmArgs a, hipStream_t s) {
+static void launch_igemm(IgemmArgs a, int splits, hipStream_t s) {
   a.tiles_o = (a.cout_p + BO - 1) / BO;
   a.nblocks = (int)(ceil_div(a.M, BP) * a.tiles_o);
-  hipLaunchKernelGGL((igemm_kernel<BF16, BO, BP, WGO, WGP, NSTAGE>), dim3(a.nblocks), dim3(64 * WGO * WGP), 0, s, a);
+  hipLaunchKernelGGL((igemm_kernel<BF16, BO, BP, WGO, WGP, NSTAGE>), dim3(a.nblocks, splits), dim3(64 * WGO * WGP), 0,
+                     s, a);
+}
+
+template <int OG>
+static void launch_g8(IgemmArgs a, hipStream_t s) {
+  a.tiles_o = (a.cout_p + G8<OG>::BO - 1) / G8<OG>::BO;
+  a.nq = a.K / 64;
+  a.nblocks = (int)(ceil_div(a.M, G8<OG>::BP) * a.tiles_o);
+  if constexpr (OG == 2) hipLaunchKernelGGL(igemm8_og2_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(igemm8_og1_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+}
+
+// ------------------------------------------------------------------------------------------------
+// launch plan: tile instance and K split.  Tile ids: 0 = f32 128x128 (2-stage); bf16: 1 = 256x256,
+// 2 = 32x256, 3 = 128x256, 4 = 128x128, 5 = 64x256 (4-stage ring), 6 = 8-phase 256x256, 7 = 8-phase 128x512.
+// IC2_IGEMM_TILE=1..7 forces a bf16 tile (tests exercise every instance on small problems),
+// IC2_IGEMM_G8N=0 keeps the cout_p <= 128 layers off the 8-phase kernel, IC2_IGEMM_SPLITK=0 disables split-K.
+struct IgPlan {
+  int tile, bo, bp, splits;
+};
+
+static bool ig_env_off(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '0';
+}
+
+static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int kw, int64_t x_elems) {
+  static const int BOs[8] = {128, 256, 32, 128, 128, 64, 256, 128};
+  static const int BPs[8] = {128, 256, 256, 256, 128, 256, 256, 512};
+  static const int forced = [] {
+    const char* e = getenv("IC2_IGEMM_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  static const bool g8n = !ig_env_off("IC2_IGEMM_G8N");
+  static const bool splitk = !ig_env_off("IC2_IGEMM_SPLITK");
+  const int64_t K = (int64_t)kh * kw * cin_p;
+  int tile = 0;
+  if (dtype == IC2_BF16) {
+    // o-tile: the widest of {256, 128, 64, 32} that divides cout_p (no padded MFMA rows), 256-pixel
+    // tiles while the grid keeps >= 2 workgroups per CU, else the 128 x 128 tile
+    const bool big_m = ceil_div(M, 256) * ((cout_p + 255) / 256) >= 512;
+    if (!big_m) tile = cout_p <= 32 ? 2 : 4;
+    else if (cout_p % 256 == 0) tile = 1;
+    else if (cout_p % 128 == 0) tile = 3;
+    else if (cout_p % 64 == 0) tile = 5;
+    else tile = 2;
+    // the 8-phase kernels wherever K-tiles are 64 deep (their buffer descriptors address < 2 GiB per
+    // operand and their tap masks hold <= 32 taps): 256 x 256 for cout_p > 128 (padded 64-row quadrants
+    // skip their MFMAs), 128 x 512 for 32 < cout_p <= 128 while the grid keeps >= 1 workgroup per CU
+    const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && x_elems * 2 < (int64_t)kOob &&
+                       (int64_t)cout_p * K * 2 < (int64_t)kOob;
+    if (big_m && cout_p > 128 && fits8) tile = 6;
+    else if (g8n && fits8 && cout_p > 32 && cout_p <= 128 && ceil_div(M, 512) >= 256) tile = 7;
+    if (forced >= 1 && forced <= 7) tile = forced;
+    if ((tile == 6 || tile == 7) && !fits8) tile = 1;
+  }
+  IgPlan pl{tile, BOs[tile], BPs[tile], 1};
+  if (tile < 6 && splitk) {
+    // fewer workgroups than ~1.25 per CU: split K so the launch reaches ~512 workgroups, each slice
+    // keeping >= 8 chunks of 32
+    const int64_t blocks = ceil_div(M, pl.bp) * ceil_div(cout_p, pl.bo);
+    const int64_t nq32 = K / 32;
+    if (blocks < 320 && M * cout_p < (1LL << 31)) {
+      int64_t sp = ceil_div(512, blocks);
+      if (sp > nq32 / 8) sp = nq32 / 8;
+      if (sp > 32) sp = 32;
+      pl.splits = sp < 1 ? 1 : (int)sp;
+    }
+  }
+  return pl;
 }
 
 }  // namespace ic2
 
 using namespace ic2;
 
-extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
-                              int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
-                              const float* oscale, const float* bias, int act, float slope, float act_gain,
-                              float clamp, float out_mul, int out_layout, void* stream) {
+extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
+                                           int pad) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
+  const int64_t M = (int64_t)n * ho * wo;
+  const IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
+  return pl.splits > 1 ? (int64_t)pl.splits * M * cout_p * 4 : 0;
+}
+
+extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
+                                 int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
+                                 const float* oscale, const float* bias, int act, float slope, float act_gain,
+                                 float clamp, float out_mul, int out_layout, void* workspace, int64_t ws_bytes,
+                                 void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
   IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_igemm: bad dtype %d", dtype);
   IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout == IC2_LAYOUT_NHWC),
@@ -550,11 +693,12 @@ extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, 
   IC2_CHECK_ARG(out_layout == IC2_LAYOUT_NHWC || (out_layout == IC2_LAYOUT_NCHW && out_dtype == IC2_F32 &&
                                                   cout_valid > 0 && cout_valid <= cout_p),
                 "conv_igemm: NCHW output needs f32 and 0 < cout_valid <= cout_p");
-  IC2_CHECK_ARG(((uintptr_t)oscale | (uintptr_t)bias) % 16 == 0, "conv_igemm: oscale/bias must be 16-byte aligned");
+  IC2_CHECK_ARG(((uintptr_t)oscale | (uintptr_t)bias | (uintptr_t)workspace) % 16 == 0,
+                "conv_igemm: oscale/bias/workspace must be 16-byte aligned");
   const int64_t M = (int64_t)n * ho * wo;
   IC2_CHECK_ARG(M < (1LL << 30), "conv_igemm: too many output pixels");
   IgemmArgs a;
-  a.x = x; a.w = w; a.y = y; a.oscale = oscale; a.bias = bias;
+  a.x = x; a.w = w; a.y = y; a.oscale = oscale; a.bias = bias; a.ws = reinterpret_cast<float*>(workspace);
   a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
   a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
@@ -567,46 +711,34 @@ extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, 
   }();
   a.group = group;
   hipStream_t s = as_stream(stream);
+  IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
+  if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   if (dtype == IC2_BF16) {
-    // the widest o-tile the layer fills; 256-pixel tiles while the grid keeps >= 2 workgroups per CU
-    // IC2_IGEMM_TILE=1..4 forces a tile (tests exercise every instance on small problems)
-    static const int forced = [] {
-      const char* e = getenv("IC2_IGEMM_TILE");
-      return e ? atoi(e) : 0;
-    }();
-    // o-tile: the widest of {256, 128, 64, 32} that divides cout_p (no padded MFMA rows), 256-pixel
-    // tiles while the grid keeps >= 2 workgroups per CU, else the 128 x 128 tile
-    const bool big_m = ceil_div(M, 256) * ((cout_p + 255) / 256) >= 512;
-    int tile;
-    if (!big_m) tile = cout_p <= 32 ? 2 : 4;
-    else if (cout_p % 256 == 0) tile = 1;
-    else if (cout_p % 128 == 0) tile = 3;
-    else if (cout_p % 64 == 0) tile = 5;
-    else tile = 2;
-    // the 8-phase 256 x 256 kernel wherever the o-tile is wider than 128 and K-tiles are 64 deep
-    // (its buffer descriptors address < 2 GiB per operand and its tap masks hold <= 32 taps)
-    const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && (int64_t)n * h * w_ * cin_p * 2 < (int64_t)kOob &&
-                       (int64_t)cout_p * a.K * 2 < (int64_t)kOob;
-    if (big_m && cout_p > 128 && fits8) tile = 6;  // even with 25 % padded rows (cout 192) it wins
-    if (forced >= 1 && forced <= 6) tile = forced;
-    if (tile == 6 && !fits8) tile = 1;
-    switch (tile) {
-      case 6: {
-        a.tiles_o = (cout_p + 255) / 256;
-        a.nq = a.K / 64;
-        a.nblocks = (int)(ceil_div(a.M, 256) * a.tiles_o);
-        hipLaunchKernelGGL(igemm8_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
-        break;
-      }
-      case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, s); break;
-      case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, s); break;
-      case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, s); break;
-      case 5: launch_igemm<true, 64, 256, 1, 4, 4>(a, s); break;
-      default: launch_igemm<true, 128, 128, 2, 2, 4>(a, s); break;
+    switch (pl.tile) {
+      case 6: launch_g8<2>(a, s); break;
+      case 7: launch_g8<1>(a, s); break;
+      case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, pl.splits, s); break;
+      case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, pl.splits, s); break;
+      case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, pl.splits, s); break;
+      case 5: launch_igemm<true, 64, 256, 1, 4, 4>(a, pl.splits, s); break;
+      default: launch_igemm<true, 128, 128, 2, 2, 4>(a, pl.splits, s); break;
     }
   } else {
-    launch_igemm<false, 128, 128, 2, 2, 2>(a, s);
+    launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
+  }
+  if (pl.splits > 1) {
+    const int64_t total = M * (cout_p / 4);
+    const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
+    hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);
   }
   IC2_CHECK_LAUNCH("conv_igemm");
   return IC2_OK;
+}
+
+extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
+                              int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
+                              const float* oscale, const float* bias, int act, float slope, float act_gain,
+                              float clamp, float out_mul, int out_layout, void* stream) {
+  return ic2_conv_igemm_ws(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo, oscale,
+                           bias, act, slope, act_gain, clamp, out_mul, out_layout, nullptr, 0, stream);
 }

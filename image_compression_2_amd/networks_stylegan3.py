@@ -150,8 +150,9 @@ class SynthesisInput(torch.nn.Module):
                 nv.stream_of(ws))
         out = torch.empty([n, S, S, cp], dtype=dt, device=dev)
         w = self.packed_weight(dt)
-        nv.call("ic2_conv_igemm", nv.ptr(feats), nv.ptr(w), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, S, S,
-                cp, cp, C, 1, 1, 0, S, S, nv.ptr(post_scale), None, 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(ws))
+        nv.conv_igemm(nv.ptr(feats), nv.ptr(w), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, S, S, cp, cp, C,
+                      1, 1, 0, S, S, nv.ptr(post_scale), None, 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(ws),
+                      feats.device)
         return out
 
     def forward(self, w):
@@ -290,16 +291,17 @@ class SynthesisLayer(torch.nn.Module):
             assert self.up_factor == 1 and self.down_factor == 1 and self.padding == [0, 0, 0, 0]
             out = torch.empty([n, self.out_channels, conv, conv], dtype=torch.float32, device=x.device)
             clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
-            nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(out), nv.dtype_code(dt), nv.F32, n, s_in, s_in,
-                    self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp),
-                    nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW, stream)
+            nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(out), nv.dtype_code(dt), nv.F32, n, s_in, s_in, self.cin_p,
+                          self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp),
+                          nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW,
+                          stream, x.device)
             return out
         # bf16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16
         ydt = torch.float16 if dt == torch.bfloat16 else dt
         y = torch.empty([n, conv, conv, self.cout_p], dtype=ydt, device=x.device)
-        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
-                self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0, 0.0,
-                1.0, -1.0, 1.0, nv.NHWC, stream)
+        nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
+                      self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
+                      0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.device)
         s_out = int(self.out_size[0])
         out = torch.empty([n, s_out, s_out, self.cout_p], dtype=dt, device=x.device)
         fu = self._fu

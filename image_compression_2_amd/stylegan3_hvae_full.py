@@ -62,8 +62,9 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
     y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
-    nv.call("ic2_conv_igemm", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.t.dtype), nv.dtype_code(dt), x.n, x.h,
-            x.w, x.c_p, cout_p, cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream)
+    nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.t.dtype), nv.dtype_code(dt), x.n, x.h, x.w,
+                  x.c_p, cout_p, cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream,
+                  x.t.device)
     return _Act(y, cout)
 
 

@@ -131,6 +131,17 @@ int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dty
                    const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
                    float out_mul, int out_layout, void* stream);
 
+/* ic2_conv_igemm with a caller-owned f32 workspace for split-K.  Launches that would not fill the
+ * chip (the encoder's 16^2 .. 2^2 blocks) split the K reduction over up to 32 slices; each slice
+ * writes f32 partial sums to the workspace and a second kernel adds them in slice order
+ * (deterministic) and applies the epilogue.  ws_bytes below the size ic2_conv_igemm_ws_bytes
+ * returns for the same geometry (0 = no split) runs unsplit.  Same contract otherwise. */
+int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad);
+int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
+                      int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
+                      const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
+                      float out_mul, int out_layout, void* workspace, int64_t ws_bytes, void* stream);
+
 /* SynthesisInput.forward Fourier features [SG3-public]: t [n][4] = affine(w); per sample the
  * rotation/translation of freqs/phases, the amplitude damping and sin(2*pi*(grid.f + phi)) * amp on a
  * size x size grid -> x_out NHWC [n][size][size][c_p].  (The trailing @ W/sqrt(C) is an ic2_conv_igemm.) */
