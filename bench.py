@@ -96,6 +96,56 @@ def algorithmic_flops_per_image(enc, G, res):
     return total
 
 
+def algorithmic_bytes_per_image(enc, G, res, esz):
+    """Compulsory HBM bytes of the igemm launches per image: each conv reads its input activation and
+    writes its output once (padded channel strides, esz bytes each; ToRGB writes 3 f32 channels).
+    Weights are per launch, not per image, and are added by the caller."""
+    p32 = lambda c: (int(c) + 31) // 32 * 32
+    total, h = 0.0, res
+    total += h * h * (p32(enc.from_rgb.in_channels) + p32(enc.from_rgb.out_channels)) * esz
+    for blk in enc.blocks:
+        if h <= 1:
+            break
+        ci, co = p32(blk.conv1.in_channels), p32(blk.conv1.out_channels)
+        total += h * h * (ci + co) * esz + h * h * (co + co) * esz
+        h = h // 2
+    S, C = int(G.synthesis.input.size[0]), p32(G.synthesis.input.channels)
+    total += 2 * S * S * C * esz
+    for L in G.synthesis.layers():
+        s_in = int(L.in_size[0])
+        s = s_in + L.conv_kernel - 1
+        out = s * s * 3 * 4 if L.is_torgb else s * s * p32(L.out_channels) * esz
+        total += s_in * s_in * p32(L.in_channels) * esz + out
+    return total
+
+
+def weight_bytes(enc, G, res, esz):
+    """Packed weight bytes of the convs one step runs, and their count (= igemm calls per step)."""
+    p32 = lambda c: (int(c) + 31) // 32 * 32
+    convs, h = [enc.from_rgb], res
+    for blk in enc.blocks:
+        if h <= 1:
+            break
+        convs += [blk.conv1, blk.conv2]
+        h = h // 2
+    tot = sum(p32(c.out_channels) * p32(c.in_channels) * c.kernel_size[0] * c.kernel_size[1] * esz for c in convs)
+    C = p32(G.synthesis.input.channels)
+    tot += C * C * esz
+    tot += sum(p32(L.out_channels) * p32(L.in_channels) * L.conv_kernel ** 2 * esz for L in G.synthesis.layers())
+    return tot, len(convs) + 1 + len(list(G.synthesis.layers()))
+
+
+def pmc_traffic(config, precision, batch):
+    """roofline.traffic: HBM bytes per igemm launch from the committed PMC run for this exact workload
+    (tools/pmc_traffic.sh; FETCH_SIZE x2 + WRITE_SIZE, KiB -> bytes), or None when there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_traffic_{config}_{precision}_b{batch}.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(res, gen_res, n_images):
     """The oracle (pure-PyTorch fp32 CPU restatement) timed on the host cores: encode + quantize + decode."""
     from oracle import encoder as oe
@@ -195,10 +245,15 @@ def main():
     }
     if not args.no_roofline and igemm_ms > 0:
         per_launch_ms = igemm_ms / n_launch
+        traffic, traffic_src = pmc_traffic(args.config, args.precision, batch)
+        esz = 2 if args.precision == "bf16" else 4
+        wb, n_conv = weight_bytes(enc, G, res, esz)
+        alg_bytes = (algorithmic_bytes_per_image(enc, G, res, esz) * batch + wb) / n_conv
         achieved = flops_img * batch * args.steps / (igemm_ms * 1e-3) / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": "ic2 igemm_kernel (all conv/modconv launches)",
                            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(achieved / peak, 4), "traffic": None,
+                           "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                           "traffic_src": traffic_src, "algorithmic_bytes_per_launch": round(alg_bytes),
                            "launches": n_launch, "avg_launch_ms": round(per_launch_ms, 4),
                            "path_frac": round(value / world * flops_img / (peak * 1e12), 4),
                            "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}

@@ -638,12 +638,16 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     else if (cout_p % 64 == 0) tile = 5;
     else tile = 2;
     // the 8-phase kernels wherever K-tiles are 64 deep (their buffer descriptors address < 2 GiB per
-    // operand and their tap masks hold <= 32 taps): 256 x 256 for cout_p > 128 (padded 64-row quadrants
-    // skip their MFMAs), 128 x 512 for 32 < cout_p <= 128 while the grid keeps >= 1 workgroup per CU
+    // operand and their tap masks hold <= 32 taps) and the grid keeps ~1 workgroup per CU (measured on the
+    // bench shapes, tools/sweep_igemm.py): 256 x 256 for cout_p > 128 (padded 64-row quadrants skip their
+    // MFMAs) unless cout_p is an odd multiple of 128 (384: the 128 x 512 tile pads nothing), 128 x 512 for
+    // 64 < cout_p <= 128; cout_p = 64 keeps the 64 x 256 tile
     const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && x_elems * 2 < (int64_t)kOob &&
                        (int64_t)cout_p * K * 2 < (int64_t)kOob;
-    if (big_m && cout_p > 128 && fits8) tile = 6;
-    else if (g8n && fits8 && cout_p > 32 && cout_p <= 128 && ceil_div(M, 512) >= 256) tile = 7;
+    const bool odd128 = cout_p % 256 == 128 && cout_p > 128;
+    if (fits8 && cout_p > 128 && !odd128 && ceil_div(M, 256) * ((cout_p + 255) / 256) >= 240) tile = 6;
+    else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) &&
+             ceil_div(M, 512) * ((cout_p + 127) / 128) >= 240) tile = 7;
     if (forced >= 1 && forced <= 7) tile = forced;
     if ((tile == 6 || tile == 7) && !fits8) tile = 1;
   }

@@ -212,7 +212,8 @@ def test_flrelu_nhwc_bf16_matches_oracle(cuda, gen256_bf16_layers, layer, c_p, i
 IGEMM_CASES = [(3, 32, 19, 1, 0), (64, 96, 12, 1, 0), (181, 128, 9, 2, 0), (512, 512, 6, 2, 0),
                (256, 362, 10, 2, 1), (96, 64, 13, 1, 2), (128, 181, 11, 2, 3), (512, 256, 7, 2, 4),
                (181, 192, 9, 2, 5), (512, 512, 6, 2, 6), (181, 256, 9, 1, 6), (128, 512, 21, 1, 6),
-               (64, 300, 10, 1, 6), (128, 128, 21, 1, 7), (64, 96, 13, 1, 7), (192, 64, 17, 0, 7)]
+               (64, 300, 10, 1, 6), (128, 128, 21, 1, 7), (64, 96, 13, 1, 7), (192, 64, 17, 0, 7),
+               (64, 362, 10, 1, 7)]
 
 
 @pytest.mark.parametrize("cin,cout,size,pad,tile", IGEMM_CASES)
