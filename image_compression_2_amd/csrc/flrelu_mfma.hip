@@ -96,6 +96,25 @@ __device__ __forceinline__ fm_f2 fm_act2(fm_f2 v, float slope, float lim) {
   return r;
 }
 
+// the same on an f16 pair, after the conversion the next MFMA needs anyway: 3 packed instructions per pair
+// (slope*v, maximum3(v, slope*v, -lim) = lrelu clamped from below, min(., lim)).  f16 rounding happens
+// before the activation instead of after it: for v >= 0 identical, for v < 0 slope*f16(v) vs f16(slope*v)
+// differ by <= 1 ulp of f16 (the operand is f16 either way).
+// Two pairs per asm block, interleaved (one block keeps the compiler from padding dependent inline-asm
+// instructions with s_nop; plain VALU RAW dependences interlock in hardware).
+__device__ __forceinline__ uint2 fm_act_h4(uint32_t h0, uint32_t h1, uint32_t slope2, uint32_t nlim2, uint32_t lim2) {
+  uint32_t t0, t1;
+  asm("v_pk_mul_f16 %2, %0, %4\n\t"
+      "v_pk_mul_f16 %3, %1, %4\n\t"
+      "v_pk_maximum3_f16 %0, %0, %2, %5\n\t"
+      "v_pk_maximum3_f16 %1, %1, %3, %5\n\t"
+      "v_pk_min_f16 %0, %0, %6\n\t"
+      "v_pk_min_f16 %1, %1, %6"
+      : "+v"(h0), "+v"(h1), "=&v"(t0), "=&v"(t1)
+      : "v"(slope2), "v"(nlim2), "v"(lim2));
+  return make_uint2(h0, h1);
+}
+
 __device__ __forceinline__ int fm_xcd_remap(int b, int nblocks) {
   const int xcd = b & 7, loc = b >> 3;
   const int q8 = nblocks >> 3, r8 = nblocks & 7;
@@ -233,6 +252,7 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
     gdv[b] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
   const float slope = a.slope, lim = a.lim;
+  const uint32_t slope2 = fm_h2u(slope, slope), lim2 = fm_h2u(lim, lim), nlim2 = fm_h2u(-lim, -lim);
   bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
 
   for (int t = slot; t < ntiles; t += gridDim.x) {
@@ -250,18 +270,31 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
 #pragma unroll
     for (int b = 0; b < G::NB; ++b) {
       // ---- vertical up: V^T[c][ky] for the 16 grid rows of block b, every input column.  Fixed trip
-      // count (unrolled, so consecutive columns' MFMA latencies overlap); the tail columns past NIN
-      // repeat column NIN-1 (identical bytes to the same place)
+      // count; the tail columns past NIN repeat column NIN-1 (identical bytes to the same place).  Issued
+      // as groups (every column's LDS read, then every MFMA, then every store) with scheduling barriers
+      // between them, so the columns' LDS and MFMA latencies overlap instead of forming one serial chain
       {
+        constexpr int NC = (NIN + 3) / 4;
         const int w0 = fm_win<U, DELTA, NIN>(16 * b);
+        fm_s4 xa[NC];
+        fm_f4 vt[NC];
 #pragma unroll
-        for (int i = 0; i < (NIN + 3) / 4; ++i) {
+        for (int i = 0; i < NC; ++i) {
           const int x = min(wave + 4 * i, NIN - 1);
-          const fm_s4 xa = fm_tr_read(in_img + (w0 + 4 * g + tq) * G::IN_PITCH + x * 8 + 2 * tp);
-          fm_f4 vt = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa), gmat[b],
-                                                           fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          FM_SETTLE(vt);
-          *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) = fm_pack4(vt[0], vt[1], vt[2], vt[3]);
+          xa[i] = fm_tr_read(in_img + (w0 + 4 * g + tq) * G::IN_PITCH + x * 8 + 2 * tp);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          vt[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa[i]), gmat[b],
+                                                        fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+          const int x = min(wave + 4 * i, NIN - 1);
+          FM_SETTLE(vt[i]);
+          *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) =
+              fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
         }
       }
       __syncthreads();
@@ -271,39 +304,73 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
       // ---- horizontal: up, activation, down, for this wave's 4 grid rows of the block (the rows past RA in
       // the last block too: finite, and weighted by zero in the vertical down; no branch, so the rows'
       // MFMA chains interleave)
+      // grouped like the vertical pass: all 12 LDS reads, all 12 up MFMAs, the activations, the 8 down
+      // MFMAs, the stores
+      fm_s4 vb[4][G::NB];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int kyl = wave + 4 * rr;
-        fm_h4 au[G::NB];
+      for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
         for (int tt = 0; tt < G::NB; ++tt) {
           const int w0 = fm_win<U, DELTA, NIN>(16 * tt);
-          const fm_s4 vb = fm_tr_read(v_img + kyl * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
-          fm_f4 u = __builtin_amdgcn_mfma_f32_16x16x16f16(gmat[tt], __builtin_bit_cast(fm_h4, vb),
-                                                          fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          FM_SETTLE(u);
-          const fm_f2 p0 = fm_act2(fm_f2{u[0], u[1]}, slope, lim);
-          const fm_f2 p1 = fm_act2(fm_f2{u[2], u[3]}, slope, lim);
-          au[tt] = fm_h4_of(fm_pack4(p0.x, p0.y, p1.x, p1.y));
+          vb[rr][tt] = fm_tr_read(v_img + (wave + 4 * rr) * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
         }
-        const uint2 a0 = __builtin_bit_cast(uint2, au[0]), a1 = __builtin_bit_cast(uint2, au[1]);
-        fm_f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a0, a1), gdh01, fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        // block 2 as a second 16x16x32 with a zero upper half: a 16x16x16 accumulating onto the 16x16x32's
-        // result one instruction later reads stale rows 0-1 of the accumulator (mixed-shape srcC hazard)
-        const uint2 a2 = __builtin_bit_cast(uint2, au[2]);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a2, make_uint2(0u, 0u)), gdh2, d, 0, 0, 0);
-        FM_SETTLE(d);
-        *reinterpret_cast<uint2*>(d_img + kyl * G::D_PITCH + li * G::D_XP + 2 * g) = fm_pack4(d[0], d[1], d[2], d[3]);
+      __builtin_amdgcn_sched_barrier(0);
+      fm_f4 u[4][G::NB];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int tt = 0; tt < G::NB; ++tt)
+          u[rr][tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmat[tt], __builtin_bit_cast(fm_h4, vb[rr][tt]),
+                                                            fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fm_h4 au[4][G::NB];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int tt = 0; tt < G::NB; ++tt) {
+          FM_SETTLE(u[rr][tt]);
+#ifdef IC2_FM_F32_ACT
+          const fm_f2 p0 = fm_act2(fm_f2{u[rr][tt][0], u[rr][tt][1]}, slope, lim);
+          const fm_f2 p1 = fm_act2(fm_f2{u[rr][tt][2], u[rr][tt][3]}, slope, lim);
+          au[rr][tt] = fm_h4_of(fm_pack4(p0.x, p0.y, p1.x, p1.y));
+#else
+          au[rr][tt] = fm_h4_of(fm_act_h4(fm_h2u(u[rr][tt][0], u[rr][tt][1]), fm_h2u(u[rr][tt][2], u[rr][tt][3]),
+                                          slope2, nlim2, lim2));
+#endif
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      fm_f4 d[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const uint2 a0 = __builtin_bit_cast(uint2, au[rr][0]), a1 = __builtin_bit_cast(uint2, au[rr][1]);
+        d[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a0, a1), gdh01, fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      // block 2 as a second 16x16x32 with a zero upper half: a 16x16x16 accumulating onto the 16x16x32's
+      // result one instruction later reads stale rows 0-1 of the accumulator (mixed-shape srcC hazard)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const uint2 a2 = __builtin_bit_cast(uint2, au[rr][2]);
+        d[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a2, make_uint2(0u, 0u)), gdh2, d[rr], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        FM_SETTLE(d[rr]);
+        *reinterpret_cast<uint2*>(d_img + (wave + 4 * rr) * G::D_PITCH + li * G::D_XP + 2 * g) =
+            fm_pack4(d[rr][0], d[rr][1], d[rr][2], d[rr][3]);
       }
       __syncthreads();
       if (b == 0) FM_DUMP(2, d_img, G::D_DW);
       // ---- vertical down: accumulate block b's 16 grid rows into this wave's 4 output columns
+      fm_s4 da[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ox = wave + 4 * i;
-        const fm_s4 da = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + ox * G::D_XP + 2 * tp);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da), gdv[b], acc[i], 0, 0, 0);
-      }
+      for (int i = 0; i < 4; ++i)
+        da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + 4 * i) * G::D_XP + 2 * tp);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[b], acc[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox)
