@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-baseline-images", type=int, default=1, help="0 disables the CPU baseline leg")
+    ap.add_argument("--cpu-baseline-images", type=int, default=3, help="0 disables the CPU baseline leg")
     ap.add_argument("--no-roofline", action="store_true")
     return ap.parse_args()
 
