@@ -2,6 +2,8 @@
 // resize helpers of the compressor API.  All HBM-bound; NHWC with padded channel stride c_p.
 #include "common.h"
 
+#include <algorithm>
+
 namespace ic2 {
 
 static int grid_1d(int64_t total, int per = 1) {
@@ -119,16 +121,25 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y
   }
 }
 
-__global__ void __launch_bounds__(256) gn_finalize_kernel(const double* __restrict__ part, int ngroups_total,
-                                                          int nchunks, double count, float eps,
-                                                          float* __restrict__ stats) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= ngroups_total) return;
+// one wave per (sample, group): lanes sum the chunk partials in a fixed strided order, then a fixed xor tree
+// (deterministic; the chunk partials of one group are contiguous, so the wave's loads coalesce)
+__global__ void __launch_bounds__(64) gn_finalize_kernel(const double* __restrict__ part, int ngroups_total,
+                                                         int nchunks, double count, float eps,
+                                                         float* __restrict__ stats) {
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x;
   double s = 0.0, q = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
-    s += part[((int64_t)i * nchunks + k) * 2 + 0];
-    q += part[((int64_t)i * nchunks + k) * 2 + 1];
+  const double* pg = part + (int64_t)i * nchunks * 2;
+  for (int k = lane; k < nchunks; k += 64) {
+    s += pg[2 * k];
+    q += pg[2 * k + 1];
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    q += __shfl_xor(q, off, 64);
+  }
+  if (lane != 0) return;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -222,6 +233,69 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y,
       f(oy, ox, res, false);
     }
     st8(out + pix * c_p + ch0, res);
+  }
+}
+
+// Sample-major variant for power-of-two channel-octet counts: blockIdx.y = sample, each thread keeps one
+// channel octet (its GN mean / scale / shift loaded once) and strides over pixels with 32-bit index math
+// (the generic kernel above pays 64-bit div/mod and 24 parameter loads per 8 outputs)
+template <typename TI, typename TO, bool POOL>
+__global__ void __launch_bounds__(256) gn_apply_oct_kernel(const TI* __restrict__ y, TO* __restrict__ out, int h,
+                                                           int w, int c_p, int c, int groups,
+                                                           const float* __restrict__ stats,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float slope) {
+  const int nn = blockIdx.y;
+  const int c8 = c_p >> 3;
+  const int oct = threadIdx.x & (c8 - 1);
+  const int ppi = 256 / c8;
+  const int prow = threadIdx.x / c8;
+  const int oh = POOL ? h / 2 : h, ow = POOL ? w / 2 : w;
+  const int ohw = oh * ow;
+  const int ch0 = oct * 8;
+  const int cpg = c / groups;
+  float mu[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int ch = ch0 + k;
+    if (ch < c) {
+      const int g = ch / cpg;
+      mu[k] = stats[((int64_t)nn * groups + g) * 2 + 0];
+      sc[k] = stats[((int64_t)nn * groups + g) * 2 + 1] * gamma[ch];
+      sh[k] = beta[ch];
+    } else {
+      mu[k] = 0.f;
+      sc[k] = 0.f;
+      sh[k] = 0.f;
+    }
+  }
+  const TI* yb = y + (int64_t)nn * h * w * c_p + ch0;
+  TO* ob = out + (int64_t)nn * ohw * c_p + ch0;
+  for (int pix = blockIdx.x * ppi + prow; pix < ohw; pix += gridDim.x * ppi) {
+    float res[8];
+    auto f = [&](int idx, bool accum) {
+      float v[8];
+      ld8(yb + (int64_t)idx * c_p, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float t = (v[k] - mu[k]) * sc[k] + sh[k];
+        t = t < 0.f ? t * slope : t;
+        res[k] = accum ? res[k] + t : t;
+      }
+    };
+    if constexpr (POOL) {
+      const int oy = pix / ow, ox = pix - oy * ow;
+      const int i0 = (2 * oy) * w + 2 * ox;
+      f(i0, false);
+      f(i0 + 1, true);
+      f(i0 + w, true);
+      f(i0 + w + 1, true);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) res[k] = res[k] / 4.f;
+    } else {
+      f(pix, false);
+    }
+    st8(ob + (int64_t)pix * c_p, res);
   }
 }
 
@@ -410,7 +484,7 @@ extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int
                        groups, nchunks, chunk_pix, part);
   else
     IC2_CHECK_ARG(false, "group_norm_stats: bad dtype");
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)ceil_div(n * groups, 256)), dim3(256), 0, s, part, n * groups,
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups,
                      nchunks, (double)hw * (c / groups), eps, stats_out);
   IC2_CHECK_LAUNCH("group_norm_stats");
   return IC2_OK;
@@ -425,9 +499,23 @@ extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dty
   const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
   const int64_t total = (int64_t)n * oh * ow * (c_p / 8);
   hipStream_t s = as_stream(stream);
+  const int c8 = c_p / 8;
+  const bool oct = c8 <= 256 && (c8 & (c8 - 1)) == 0 && (int64_t)h * w < (1LL << 31) / c_p;
+  const int ohw = oh * ow;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ohw, 256 / std::max(c8, 1)),
+                                                                        ceil_div(4096, n)));
 #define IC2_GN_LAUNCH(TI, TO)                                                                                     \
-  hipLaunchKernelGGL((gn_apply_kernel<TI, TO>), dim3(grid_1d(total)), dim3(256), 0, s, (const TI*)y, (TO*)out, n, h, \
-                     w, c_p, c, groups, stats, gamma, beta, slope, pool)
+  do {                                                                                                          \
+  if (oct && pool)                                                                                              \
+    hipLaunchKernelGGL((gn_apply_oct_kernel<TI, TO, true>), dim3(gx, (unsigned)n), dim3(256), 0, s, (const TI*)y,  \
+                       (TO*)out, h, w, c_p, c, groups, stats, gamma, beta, slope);                              \
+  else if (oct)                                                                                                 \
+    hipLaunchKernelGGL((gn_apply_oct_kernel<TI, TO, false>), dim3(gx, (unsigned)n), dim3(256), 0, s, (const TI*)y, \
+                       (TO*)out, h, w, c_p, c, groups, stats, gamma, beta, slope);                              \
+  else                                                                                                          \
+    hipLaunchKernelGGL((gn_apply_kernel<TI, TO>), dim3(grid_1d(total)), dim3(256), 0, s, (const TI*)y, (TO*)out, n, \
+                       h, w, c_p, c, groups, stats, gamma, beta, slope, pool);                          \
+  } while (0)
   if (dtype_in == IC2_F32 && dtype_out == IC2_F32) IC2_GN_LAUNCH(float, float);
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(bf16_t, bf16_t);
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_F32) IC2_GN_LAUNCH(bf16_t, float);

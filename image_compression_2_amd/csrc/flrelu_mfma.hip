@@ -17,6 +17,8 @@
 // workgroups loop over tiles and prefetch the next tile's input (LDS-DMA) while finishing the current one.
 #include "flrelu.h"
 
+#include <cstdlib>
+
 namespace ic2 {
 
 typedef _Float16 fm_h2 __attribute__((ext_vector_type(2)));
@@ -45,6 +47,9 @@ struct FmGeom {
   static constexpr int D_PITCH = 16 * D_XP + 8;        // 168 = 40 mod 64: 8 rows hit 8 bank groups
   static constexpr int D_DW = 16 * D_PITCH;
   static constexpr int LDS_DW = IN_DW + V_DW + D_DW + FM_TAPS;
+  // V and D sharing one region (two more barriers per grid block): 38.6 KB for up 2, i.e. 4 workgroups per CU
+  static constexpr int VD_DW = V_DW > D_DW ? V_DW : D_DW;
+  static constexpr int LDS_DW_ALIAS = IN_DW + VD_DW + FM_TAPS;
   static_assert(NIN % 2 == 1 && NIN >= 16, "input image width must be odd and cover a 16-wide window");
 };
 
@@ -133,15 +138,16 @@ extern "C" int ic2_fm_debug_fetch(uint32_t* host, int which) {
 #define FM_DUMP(which, ptr, ndw) (void)0
 #endif
 
-template <int U, int DELTA, bool IN_F16>
+template <int U, int DELTA, bool IN_F16, bool ALIAS>
 __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles) {
   using G = FmGeom<U>;
   constexpr int NIN = G::NIN, NCH = NIN * NIN * 2;  // input pixels x 16-B halves
-  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[ALIAS ? G::LDS_DW_ALIAS : G::LDS_DW];
   uint32_t* const in_img = lds;
   uint32_t* const v_img = lds + G::IN_DW;
-  uint32_t* const d_img = v_img + G::V_DW;
-  float* const taps = reinterpret_cast<float*>(d_img + G::D_DW);  // FM_TAPS floats, layout below
+  uint32_t* const d_img = ALIAS ? v_img : v_img + G::V_DW;
+  // FM_TAPS floats, layout below
+  float* const taps = reinterpret_cast<float*>(v_img + (ALIAS ? G::VD_DW : G::V_DW + G::D_DW));
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -289,6 +295,11 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
           vt[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa[i]), gmat[b],
                                                         fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+        // V overwrites D: every wave's vertical-down reads of the previous block are done (block 0: the
+        // tile-top barrier already separates them)
+        if constexpr (ALIAS) {
+          if (b > 0) __syncthreads();
+        }
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
           const int x = min(wave + 4 * i, NIN - 1);
@@ -353,6 +364,7 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
         d[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a2, make_uint2(0u, 0u)), gdh2, d[rr], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (ALIAS) __syncthreads();  // D overwrites V: every wave's horizontal reads are done
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         FM_SETTLE(d[rr]);
@@ -392,19 +404,33 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
   }
 }
 
-template <int U, int DELTA, bool IN_F16>
-static void fm_launch_one(const FlrArgs& a, int ntiles, hipStream_t s) {
+template <int U, int DELTA, bool IN_F16, bool ALIAS>
+static void fm_launch_alias(const FlrArgs& a, int ntiles, hipStream_t s) {
   // persistent grid: every CU filled to the kernel's occupancy, capped by the tile count
   static int resident = 0;
   if (resident == 0) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma_kernel<U, DELTA, IN_F16>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS>, 256, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((flrelu_mfma_kernel<U, DELTA, IN_F16>), dim3((unsigned)grid), dim3(256), 0, s, a, ntiles);
+  hipLaunchKernelGGL((flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS>), dim3((unsigned)grid), dim3(256), 0, s, a, ntiles);
+}
+
+// IC2_FLR_ALIAS=0/1 selects the separate-V/D (3 workgroups per CU, default) or the aliased (4 per CU) LDS
+// layout for up 2; up 4 (30.5 KB) already fits 5 workgroups and keeps the separate layout.  Measured on the
+// bench (batch 32): 1180 vs 1185 img/s -- the extra barriers cancel the occupancy gain, so the kernel is
+// not occupancy-bound.
+template <int U, int DELTA, bool IN_F16>
+static void fm_launch_one(const FlrArgs& a, int ntiles, hipStream_t s) {
+  static const int alias = [] {
+    const char* e = getenv("IC2_FLR_ALIAS");
+    return e ? atoi(e) : 0;
+  }();
+  if (U == 2 && alias) fm_launch_alias<U, DELTA, IN_F16, true>(a, ntiles, s);
+  else fm_launch_alias<U, DELTA, IN_F16, false>(a, ntiles, s);
 }
 
 template <bool IN_F16>

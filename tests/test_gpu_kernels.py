@@ -271,7 +271,9 @@ def test_fc_matches_torch(cuda, n, in_f, out_f, ldx, act):
 
 # ------------------------------------------------------------------ GroupNorm + lrelu (+ pool), fp32 reference
 @pytest.mark.parametrize("n,c,groups,h,w,pool", [(2, 64, 32, 5, 7, True), (3, 96, 32, 9, 6, False),
-                                                 (32, 512, 32, 2, 2, True), (1, 32, 32, 40, 33, True)])
+                                                 (32, 512, 32, 2, 2, True), (1, 32, 32, 40, 33, True),
+                                                 (4, 128, 32, 64, 64, False), (2, 256, 32, 33, 31, False),
+                                                 (2, 64, 32, 130, 128, True)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_group_norm_lrelu_pool_matches_torch(cuda, n, c, groups, h, w, pool, dtype):
     from image_compression_2_amd.stylegan3_hvae_full import _group_norm_lrelu
