@@ -162,3 +162,13 @@ def torch_dtype(precision):
 
 def pad32(c):
     return (int(c) + 31) // 32 * 32
+
+
+def pad_synth(c):
+    """Synthesis activation channel stride: multiple of 32 up to 128 channels, of 64 above.  The SG3-T-1024
+    widths 323 / 203 then land on 384 / 256, whose K-chunks are 64 deep and whose o-tiles are 128 / 256 wide,
+    so those layers run on the 8-phase MFMA kernels instead of the 32-row tile (measured: L8_276_203 2.33 ms
+    at batch 8 on the 352 / 224 strides); 81 / 51 keep 96 / 64 (the filtered-lrelu pays for every padded
+    channel).  The SG3-T-256 strides (181 -> 192, 362 -> 384) are unchanged."""
+    c = int(c)
+    return pad32(c) if c <= 128 else (c + 63) // 64 * 64

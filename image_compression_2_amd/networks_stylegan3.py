@@ -131,7 +131,7 @@ class SynthesisInput(torch.nn.Module):
         hit = self._cache.get(dt)
         if hit is not None and hit[0] == key:
             return hit[1]
-        C, cp = self.channels, nv.pad32(self.channels)
+        C, cp = self.channels, nv.pad_synth(self.channels)
         w = self.weight.detach().to(torch.float32).contiguous()
         out = torch.empty([cp, cp], dtype=dt, device=w.device)
         nv.call("ic2_pack_weight", nv.ptr(w), C, C, 1, 1, cp, cp, 0, float(1 / np.sqrt(C)), nv.ptr(out),
@@ -141,7 +141,7 @@ class SynthesisInput(torch.nn.Module):
 
     def run_nhwc(self, ws, ldx, n, dt, post_scale):
         """Features -> NHWC [n, S, S, c_p] (dt), scaled by the first layer's xscale (post_scale)."""
-        C, cp, S = self.channels, nv.pad32(self.channels), int(self.size[0])
+        C, cp, S = self.channels, nv.pad_synth(self.channels), int(self.size[0])
         dev = ws.device
         t = self.affine.run(ws, ldx=ldx, n=n)
         feats = torch.empty([n, S, S, cp], dtype=dt, device=dev)
@@ -158,7 +158,7 @@ class SynthesisInput(torch.nn.Module):
     def forward(self, w):
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(w)
-        n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad32(self.channels)
+        n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad_synth(self.channels)
         x = self.run_nhwc(w, self.w_dim, n, torch.float32, None)
         y = torch.empty([n, C, S, S], dtype=torch.float32, device=w.device)
         nv.call("ic2_nhwc_to_nchw", nv.ptr(x), nv.F32, nv.ptr(y), n, C, S, S, cp, nv.stream_of(w))
@@ -233,11 +233,11 @@ class SynthesisLayer(torch.nn.Module):
     # ---- constants -------------------------------------------------------------------------
     @property
     def cin_p(self):
-        return nv.pad32(self.in_channels)
+        return nv.pad_synth(self.in_channels)
 
     @property
     def cout_p(self):
-        return nv.pad32(self.out_channels)
+        return nv.pad_synth(self.out_channels)
 
     def input_gain(self):
         key = _version_key(self.magnitude_ema)

@@ -91,6 +91,65 @@ def test_batch_shard_changes_only_rounding(cuda, gen256):
     assert _maxdiff(full, parts) < 1e-4
 
 
+# ------------------------------------------------------------------ SG3-T-1024 (BASELINE config C4)
+@pytest.fixture(scope="module")
+def gen1024(cuda):
+    torch.manual_seed(11)
+    return ic2.Generator(img_resolution=1024).to(cuda).eval()
+
+
+def test_synthesis_1024_fp32_within_1e3_of_oracle(cuda, gen1024):
+    """C4 geometry (L0_36_512 ... L14_1024_3: up-4 layers at 276/532/1044, the 1044 -> 1024 crop, 32-channel
+    tail) through the whole network, fp32 mode, against the fp32 CPU restatement -- the reference's own CPU
+    precision -- at the north-star 1e-3 max-abs bar."""
+    sd = _sd_cpu(gen1024)
+    ws = torch.randn(1, 16, 512, generator=torch.Generator().manual_seed(12)) * 0.7
+    img = gen1024.synthesis(ws.to(cuda), noise_mode="const")
+    ref = sg3.synthesis_forward(sd, 1024, ws, dtype=torch.float32)
+    assert img.shape == (1, 3, 1024, 1024) and img.dtype == torch.float32
+    assert _maxdiff(img, ref) < 1e-3
+
+
+def test_synthesis_1024_bf16_psnr_close_to_fp32(cuda, gen1024):
+    """The bf16 throughput mode at 1024^2: PSNR against a target within 0.01 dB of the fp32 mode's."""
+    ws = torch.randn(2, 16, 512, generator=torch.Generator().manual_seed(13)).to(cuda) * 0.7
+    target = (torch.rand(2, 3, 1024, 1024, generator=torch.Generator().manual_seed(14)) * 2 - 1).to(cuda)
+    gen1024.set_precision("fp32")
+    a = gen1024.synthesis(ws)
+    gen1024.set_precision("bf16")
+    try:
+        b = gen1024.synthesis(ws)
+    finally:
+        gen1024.set_precision("fp32")
+    rel = (a - b).abs().max().item() / (a.abs().max().item() + 1e-6)
+    assert rel < 0.08
+    assert abs(icm.psnr(a, target) - icm.psnr(b, target)) < 0.01
+
+
+def test_compress_decompress_1024_round_trip(cuda, gen1024):
+    """C4 end to end (1024-config encoder on 1024^2 input, 8-bit quantize, SG3-T-1024 decode), bf16: the
+    quantized latents index-exact against the oracle quantizer on the same means, the decode deterministic."""
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision="bf16").to(cuda).eval()
+    comp = ic2.StyleGAN3Compressor(enc, gen1024)
+    x = (torch.rand(2, 3, 1024, 1024, generator=torch.Generator().manual_seed(15)) * 2 - 1).to(cuda)
+    gen1024.set_precision("bf16")
+    try:
+        with torch.no_grad():
+            torch.manual_seed(5)   # the fine projector re-draws fc1 from the CPU RNG on every call (ref :225-230)
+            q = comp.compress(x, quantization_bits=8, deterministic=True)
+            torch.manual_seed(5)
+            _, means, _ = enc(x)
+            img1 = comp.decompress(q)
+            img2 = comp.decompress(q)
+    finally:
+        gen1024.set_precision("fp32")
+    assert q.shape == (2, 16, 512)
+    assert torch.equal(q.cpu(), oe.quantize_uniform(means.cpu(), 8))
+    assert img1.shape == (2, 3, 1024, 1024) and torch.isfinite(img1).all()
+    assert torch.equal(img1, img2)
+
+
 # ------------------------------------------------------------------ encoder vs the reference's goldens
 def test_encoder_small_matches_reference(cuda, golden_dir):
     d = np.load(os.path.join(golden_dir, "encoder_small.npz"))
