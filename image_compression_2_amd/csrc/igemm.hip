@@ -667,6 +667,157 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
   return pl;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Halo direct conv for narrow 3x3 layers (cin_p <= 96, cout_p <= 64; bf16): the encoder's block 0 and from_rgb
+// and the SG3-T-1024 tail (L11_1044_51, L12_1044_32, L13_1024_32) at >= 256^2.  There the implicit GEMM above re-fetches
+// every input pixel once per tap (9 shifted 256-pixel panels per 32 channels) for only 32-64 MACs per
+// fetched element, and its per-chunk barrier guards 8-16 MFMAs.  Here a persistent workgroup keeps the
+// whole packed weight [cout_p][9][cin_p] in LDS, stages one (TH+2) x (32+2) x cin_p input halo per
+// TH x 32-pixel output tile (TH = 8, or 4 at 96 channels; fetched once: 1.6x instead of 9x), and runs all 9 * cin_p/32 K-steps without
+// a barrier.  The next tile's halo is loaded into registers while the current tile computes.
+// Wave w of 8 owns pixel blocks {w, w+8, ...} (16 pixels of one row) x every 16-channel o-block:
+// A = weights (lane: o = 16i + fr, k = 8 fh .. +7), B = halo pixels (lane: pixel fr, k = 8 fh .. +7).
+// Epilogue = ig_store4 (same oscale / bias / activation / output layouts as the implicit GEMM).
+template <int CINP, int COUTP, int TH>
+struct HcCfg {
+  static constexpr int TW = 32, HR = TH + 2, HC = TW + 2;
+  static constexpr int PPB = CINP * 2 + 16;          // halo pixel pitch (bytes): 16 lanes hit distinct banks
+  static constexpr int WPB = 9 * CINP * 2 + 16;      // weight row pitch (bytes)
+  static constexpr int HALO_B = HR * HC * PPB, W_B = COUTP * WPB;
+  static constexpr int CB = CINP / 32, OB = COUTP / 16, JB = TH * 2 / 8;
+  static constexpr int NPIECE = HR * HC * (CINP / 8);  // 16-B pieces per halo
+  static constexpr int PER_T = (NPIECE + 511) / 512;
+};
+
+template <int CINP, int COUTP, int TH>
+__global__ void __launch_bounds__(512) hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
+  using C = HcCfg<CINP, COUTP, TH>;
+  __shared__ __attribute__((aligned(16))) char lds[C::HALO_B + C::W_B];
+  char* const halo = lds;
+  char* const wts = lds + C::HALO_B;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+
+  // packed weight -> LDS, once per workgroup
+  const char* wg = reinterpret_cast<const char*>(a.w);
+  constexpr int WPIECE = 9 * CINP / 8;
+  for (int e = tid; e < COUTP * WPIECE; e += 512) {
+    const int o = e / WPIECE, r = e - o * WPIECE;
+    *reinterpret_cast<uint4*>(wts + o * C::WPB + r * 16) =
+        *reinterpret_cast<const uint4*>(wg + ((int64_t)o * 9 * CINP + r * 8) * 2);
+  }
+
+  const char* xg = reinterpret_cast<const char*>(a.x);
+  uint4 pre[C::PER_T];
+  auto fetch = [&](int t) {
+    const int tx = t % tiles_x;
+    const int t2 = t / tiles_x;
+    const int ty = t2 % tiles_y;
+    const int nn = t2 / tiles_y;
+    const int y0 = ty * TH - a.pad, x0 = tx * C::TW - a.pad;
+#pragma unroll
+    for (int k = 0; k < C::PER_T; ++k) {
+      const int e = tid + 512 * k;
+      const int pi = e / (CINP / 8), part = e - pi * (CINP / 8);
+      const int hr = pi / C::HC, hc = pi - hr * C::HC;
+      const int iy = y0 + hr, ix = x0 + hc;
+      const bool ok = e < C::NPIECE && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
+      pre[k] = ok ? *reinterpret_cast<const uint4*>(xg + ((((int64_t)nn * a.h + iy) * a.w_ + ix) * CINP + part * 8) * 2)
+                  : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  if (blockIdx.x < ntiles) fetch(blockIdx.x);
+
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's halo reads (and the weight stores) are done
+#pragma unroll
+    for (int k = 0; k < C::PER_T; ++k) {
+      const int e = tid + 512 * k;
+      if (e < C::NPIECE) {
+        const int pi = e / (CINP / 8), part = e - pi * (CINP / 8);
+        *reinterpret_cast<uint4*>(halo + pi * C::PPB + part * 16) = pre[k];
+      }
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);  // in flight during this tile's MFMAs
+
+    f32x4 acc[C::OB][C::JB];
+#pragma unroll
+    for (int i = 0; i < C::OB; ++i)
+#pragma unroll
+      for (int j = 0; j < C::JB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+      for (int cb = 0; cb < C::CB; ++cb) {
+        bf16x8 bfr[C::JB], af[C::OB];
+#pragma unroll
+        for (int j = 0; j < C::JB; ++j) {
+          const int pb = wave + 8 * j;
+          const int r = pb >> 1, c0 = (pb & 1) * 16;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(halo + ((r + ky) * C::HC + c0 + kx + fr) * C::PPB + cb * 64 +
+                                                    fh * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < C::OB; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(wts + (16 * i + fr) * C::WPB + (tap * CINP + cb * 32) * 2 + fh * 16);
+#pragma unroll
+        for (int i = 0; i < C::OB; ++i)
+#pragma unroll
+          for (int j = 0; j < C::JB; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    const int tx = t % tiles_x;
+    const int t2 = t / tiles_x;
+    const int ty = t2 % tiles_y;
+    const int nn = t2 / tiles_y;
+#pragma unroll
+    for (int j = 0; j < C::JB; ++j) {
+      const int pb = wave + 8 * j;
+      const int oy = ty * TH + (pb >> 1), ox = tx * C::TW + (pb & 1) * 16 + fr;
+      if (oy >= a.ho || ox >= a.wo) continue;
+      const int pix = oy * a.wo + ox;
+      const int p = nn * a.ho * a.wo + pix;
+#pragma unroll
+      for (int i = 0; i < C::OB; ++i) {
+        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        ig_store4(a, p, nn, pix, 16 * i + 4 * fh, v);
+      }
+    }
+  }
+}
+
+template <int CINP, int COUTP>
+static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
+  constexpr int TH = CINP > 64 ? 4 : 8;  // 96 channels: 4-row tiles keep halo + weight within 160 KB of LDS
+  const int tiles_x = (int)ceil_div(a.wo, 32), tiles_y = (int)ceil_div(a.ho, TH);
+  const int ntiles = a.n * tiles_x * tiles_y;
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hconv_kernel<CINP, COUTP, TH>, 512, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL((hconv_kernel<CINP, COUTP, TH>), dim3((unsigned)grid), dim3(512), 0, s, a, tiles_x, tiles_y,
+                     ntiles);
+}
+
+// the halo kernel for bf16 3x3 convs with cin_p in {32, 64, 96}, cout_p in {32, 64} and >= 64K output
+// pixels; IC2_HCONV=0 keeps them on the implicit GEMM
+static bool hconv_eligible(int dtype, int64_t M, int cin_p, int cout_p, int kh, int kw) {
+  static const bool on = !ig_env_off("IC2_HCONV");
+  return on && dtype == IC2_BF16 && kh == 3 && kw == 3 && (cin_p == 32 || cin_p == 64 || cin_p == 96) &&
+         (cout_p == 32 || cout_p == 64) && M >= 65536;
+}
+
 }  // namespace ic2
 
 using namespace ic2;
@@ -717,7 +868,14 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   hipStream_t s = as_stream(stream);
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
-  if (dtype == IC2_BF16) {
+  if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
+    if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
+    else if (cin_p == 32) launch_hconv<32, 64>(a, s);
+    else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
+    else if (cin_p == 64) launch_hconv<64, 64>(a, s);
+    else if (cout_p == 32) launch_hconv<96, 32>(a, s);
+    else launch_hconv<96, 64>(a, s);
+  } else if (dtype == IC2_BF16) {
     switch (pl.tile) {
       case 6: launch_g8<2>(a, s); break;
       case 7: launch_g8<1>(a, s); break;
@@ -730,7 +888,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   } else {
     launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
   }
-  if (pl.splits > 1) {
+  if (pl.splits > 1 && !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
     const int64_t total = M * (cout_p / 4);
     const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
     hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);

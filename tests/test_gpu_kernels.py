@@ -232,6 +232,15 @@ def test_conv_igemm(cuda, cin, cout, size, pad, tile, dtype, monkeypatch):
     _conv_case(cin, cout, size, pad, dtype)
 
 
+@pytest.mark.parametrize("cin,cout,size,pad", [(32, 32, 150, 1), (3, 32, 160, 1), (32, 64, 151, 2), (64, 32, 149, 2),
+                                              (64, 64, 149, 1), (60, 50, 150, 0), (81, 51, 150, 2), (96, 32, 149, 1)])
+def test_conv_halo_kernel(cuda, cin, cout, size, pad):
+    """The halo direct conv (bf16 3x3, cin_p / cout_p in {32, 64}, >= 64K output pixels: encoder block 0,
+    SG3-T-1024 L12/L13) against F.conv2d in fp64, with ragged 8 x 32 tiles at the right / bottom edges."""
+    assert 3 * (size + 2 * pad - 2) ** 2 >= 65536
+    _conv_case(cin, cout, size, pad)
+
+
 def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16):
     cuda = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(cin + cout)

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "1024" > gpurun_out/pytest_c4.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "1024 or halo" > gpurun_out/pytest_c4.log 2>&1
 rc=$?
 tail -6 gpurun_out/pytest_c4.log
 if [ $rc -ne 0 ]; then echo "pytest failed ($rc): stopping"; exit $rc; fi
