@@ -818,6 +818,73 @@ static bool hconv_eligible(int dtype, int64_t M, int cin_p, int cout_p, int kh, 
          (cout_p == 32 || cout_p == 64) && M >= 65536;
 }
 
+// ------------------------------------------------------------------------------------------------
+// ToRGB (1x1 conv to <= 4 channels, NCHW f32 output; SG3 SynthesisLayer L14, is_torgb): HBM-bound, so a
+// VALU dot product instead of a 32-row MFMA tile that is 29/32 padding.  L = cin_p/16 lanes per pixel,
+// 16 channels (2 x 16 B) each, a fixed xor-shuffle tree over the L lanes, then the igemm epilogue math
+// (oscale, bias, activation / clamp, out_mul) on the group's first lane.
+template <int L, int CV>
+__global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
+  const int tid = blockIdx.x * 256 + threadIdx.x;
+  const int sub = threadIdx.x & (L - 1);
+  const int hw = a.ho * a.wo;
+  float wv[CV][16];
+  const uint16_t* wg = reinterpret_cast<const uint16_t*>(a.w);
+#pragma unroll
+  for (int o = 0; o < CV; ++o)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wv[o][k] = __uint_as_float((uint32_t)wg[(int64_t)o * a.cin_p + sub * 16 + k] << 16);
+  float bi[CV];
+#pragma unroll
+  for (int o = 0; o < CV; ++o) bi[o] = a.bias ? a.bias[o] : 0.f;
+  const uint16_t* xg = reinterpret_cast<const uint16_t*>(a.x);
+  float* yo = reinterpret_cast<float*>(a.y);
+  const int stride = gridDim.x * (256 / L);
+  for (int p = tid / L; p < a.M; p += stride) {
+    const uint4* src = reinterpret_cast<const uint4*>(xg + (int64_t)p * a.cin_p + sub * 16);
+    const uint4 u0 = src[0], u1 = src[1];
+    const uint32_t w32[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    float acc[CV];
+#pragma unroll
+    for (int o = 0; o < CV; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float lo = __uint_as_float(w32[k] << 16), hi = __uint_as_float(w32[k] & 0xffff0000u);
+#pragma unroll
+      for (int o = 0; o < CV; ++o) acc[o] = fmaf(wv[o][2 * k + 1], hi, fmaf(wv[o][2 * k], lo, acc[o]));
+    }
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1)
+#pragma unroll
+      for (int o = 0; o < CV; ++o) acc[o] += __shfl_xor(acc[o], m, 64);
+    if (sub == 0) {
+      const int nn = p / hw, pix = p - nn * hw;
+#pragma unroll
+      for (int o = 0; o < CV; ++o) {
+        if (o >= a.cout_valid) break;
+        float t = acc[o] * (a.oscale ? a.oscale[(int64_t)nn * a.cout_p + o] : 1.f) + bi[o];
+        if (a.act) t = lrelu_gain_clamp(t, a.slope, a.act_gain, a.clamp);
+        yo[((int64_t)nn * a.cout_valid + o) * hw + pix] = t * a.out_mul;
+      }
+    }
+  }
+}
+
+static bool torgb_eligible(int dtype, int cin_p, int cout_valid, int kh, int kw, int out_layout, int out_dtype) {
+  static const bool on = !ig_env_off("IC2_TORGB");
+  return on && dtype == IC2_BF16 && kh == 1 && kw == 1 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
+         out_dtype == IC2_F32 && (cin_p == 32 || cin_p == 64 || cin_p == 128);
+}
+
+static void launch_torgb(const IgemmArgs& a, hipStream_t s) {
+  const int L = a.cin_p / 16;
+  const int64_t need = ceil_div((int64_t)a.M * L, 256);
+  const unsigned grid = (unsigned)(need < 8192 ? need : 8192);
+  if (L == 2) hipLaunchKernelGGL((torgb_kernel<2, 4>), dim3(grid), dim3(256), 0, s, a);
+  else if (L == 4) hipLaunchKernelGGL((torgb_kernel<4, 4>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((torgb_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a);
+}
+
 }  // namespace ic2
 
 using namespace ic2;
@@ -868,7 +935,10 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   hipStream_t s = as_stream(stream);
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
-  if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
+  const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, out_layout, out_dtype);
+  if (torgb) {
+    launch_torgb(a, s);
+  } else if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
     if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
     else if (cin_p == 32) launch_hconv<32, 64>(a, s);
     else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
@@ -888,7 +958,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   } else {
     launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
   }
-  if (pl.splits > 1 && !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
+  if (pl.splits > 1 && !torgb && !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
     const int64_t total = M * (cout_p / 4);
     const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
     hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);

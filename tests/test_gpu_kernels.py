@@ -241,6 +241,25 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad):
     _conv_case(cin, cout, size, pad)
 
 
+@pytest.mark.parametrize("cin_p,n,size", [(32, 2, 67), (64, 1, 40), (128, 3, 33)])
+def test_torgb_1x1_nchw(cuda, cin_p, n, size):
+    """ToRGB (1x1 conv to 3 channels, bf16 NHWC in, NCHW f32 out with per-sample oscale, bias, clamp and
+    out_mul: the SynthesisLayer L14 call) against an fp64 reference on the same bf16 operands."""
+    g = torch.Generator().manual_seed(cin_p + size)
+    x = (torch.randn(n, size, size, cin_p, generator=g) * 3).to(torch.bfloat16)
+    w = (torch.randn(32, cin_p, generator=g) / np.sqrt(cin_p)).to(torch.bfloat16)
+    osc = torch.rand(n, 32, generator=g) + 0.5
+    bias = torch.randn(32, generator=g)
+    y = torch.empty(n, 3, size, size, device=cuda)
+    xd, wd, od, bd = x.to(cuda), w.to(cuda), osc.to(cuda), bias.to(cuda)
+    nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), nv.BF16, nv.F32, n, size, size, cin_p, 32, 3, 1, 1, 0, size,
+                  size, nv.ptr(od), nv.ptr(bd), nv.ACT_LRELU, 1.0, 1.0, 8.0, 0.25, nv.NCHW, nv.stream_of(xd), cuda)
+    torch.cuda.synchronize()
+    acc = torch.einsum("nhwc,oc->nohw", x.double(), w.double()[:3])
+    r = (acc * osc.double()[:, :3, None, None] + bias.double()[None, :3, None, None]).clamp(-8, 8) * 0.25
+    assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item())
+
+
 def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16):
     cuda = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(cin + cout)
