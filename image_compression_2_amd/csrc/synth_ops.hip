@@ -243,45 +243,46 @@ __global__ void __launch_bounds__(256) oscale_kernel(const float* __restrict__ x
 // ------------------------------------------------------------------------------------------------
 // SynthesisInput Fourier features (NHWC)
 // ------------------------------------------------------------------------------------------------
+// one workgroup per (sample, row): each thread owns channels tid, tid + 256, ... and derives their rotated
+// frequency, phase and amplitude once, then walks the row (stores coalesced along channels)
 template <typename T>
 __global__ void __launch_bounds__(256) synth_input_kernel(const float* __restrict__ t, const float* __restrict__ freqs,
                                                           const float* __restrict__ phases,
                                                           const float* __restrict__ tr, int n, int c, int c_p,
                                                           int size, float sr, float bw, T* __restrict__ out) {
-  const int64_t total = (int64_t)n * size * size * c_p;
+  const int nn = blockIdx.x / size, yy = blockIdx.x - (blockIdx.x / size) * size;
   const float theta = 0.5f * (float)size / sr;
   const float two_pi = 6.283185307179586f;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int ch = (int)(e % c_p);
-    const int64_t pix = e / c_p;
-    const int xx = (int)(pix % size);
-    const int yy = (int)((pix / size) % size);
-    const int nn = (int)(pix / ((int64_t)size * size));
+  // t' = t / |t[:2]|
+  const float* tn = t + nn * 4;
+  const float nrm = sqrtf(tn[0] * tn[0] + tn[1] * tn[1]);
+  const float rc = tn[0] / nrm, rs = tn[1] / nrm, tx = tn[2] / nrm, ty = tn[3] / nrm;
+  // m_r @ m_t, then @ user transform tr (3x3)
+  const float A[3][3] = {{rc, -rs, -rc * tx + rs * ty}, {rs, rc, -rs * tx - rc * ty}, {0.f, 0.f, 1.f}};
+  float M[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) M[r][q] = A[r][0] * tr[0 * 3 + q] + A[r][1] * tr[1 * 3 + q] + A[r][2] * tr[2 * 3 + q];
+  // affine_grid(align_corners=False): base coordinate (2j+1)/size - 1, scaled by theta
+  const float gy = ((2.f * yy + 1.f) / (float)size - 1.f) * theta;
+  T* orow = out + ((int64_t)nn * size + yy) * size * c_p;
+  for (int ch = threadIdx.x; ch < c_p; ch += 256) {
     if (ch >= c) {
-      st(out + e, 0.f);
+      for (int xx = 0; xx < size; ++xx) st(orow + (int64_t)xx * c_p + ch, 0.f);
       continue;
     }
-    // t' = t / |t[:2]|
-    const float* tn = t + nn * 4;
-    const float nrm = sqrtf(tn[0] * tn[0] + tn[1] * tn[1]);
-    const float rc = tn[0] / nrm, rs = tn[1] / nrm, tx = tn[2] / nrm, ty = tn[3] / nrm;
-    // m_r @ m_t, then @ user transform tr (3x3)
-    const float A[3][3] = {{rc, -rs, -rc * tx + rs * ty}, {rs, rc, -rs * tx - rc * ty}, {0.f, 0.f, 1.f}};
-    float M[3][3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) M[r][q] = A[r][0] * tr[0 * 3 + q] + A[r][1] * tr[1 * 3 + q] + A[r][2] * tr[2 * 3 + q];
     const float f0 = freqs[ch * 2 + 0], f1 = freqs[ch * 2 + 1];
     const float ph = phases[ch] + (f0 * M[0][2] + f1 * M[1][2]);
     const float g0 = f0 * M[0][0] + f1 * M[1][0];
     const float g1 = f0 * M[0][1] + f1 * M[1][1];
     const float amp = fminf(fmaxf(1.f - (sqrtf(g0 * g0 + g1 * g1) - bw) / (sr * 0.5f - bw), 0.f), 1.f);
-    // affine_grid(align_corners=False): base coordinate (2j+1)/size - 1, scaled by theta
-    const float gx = ((2.f * xx + 1.f) / (float)size - 1.f) * theta;
-    const float gy = ((2.f * yy + 1.f) / (float)size - 1.f) * theta;
-    const float arg = (gx * g0 + gy * g1) + ph;
-    st(out + e, sinf(arg * two_pi) * amp);
+    const float rowc = gy * g1;
+    for (int xx = 0; xx < size; ++xx) {
+      const float gx = ((2.f * xx + 1.f) / (float)size - 1.f) * theta;
+      const float arg = (gx * g0 + rowc) + ph;
+      st(orow + (int64_t)xx * c_p + ch, sinf(arg * two_pi) * amp);
+    }
   }
 }
 
@@ -403,13 +404,12 @@ extern "C" int ic2_synth_input_features(const float* t, const float* freqs, cons
                                         void* x_out, int dtype, void* stream) {
   IC2_CHECK_ARG(t && freqs && phases && transform && x_out && n > 0 && c > 0 && c_p >= c && size > 0,
                 "synth_input_features: bad arguments");
-  const int64_t total = (int64_t)n * size * size * c_p;
   hipStream_t s = as_stream(stream);
   if (dtype == IC2_F32)
-    hipLaunchKernelGGL(synth_input_kernel<float>, dim3(grid_1d(total)), dim3(256), 0, s, t, freqs, phases, transform,
+    hipLaunchKernelGGL(synth_input_kernel<float>, dim3((unsigned)(n * size)), dim3(256), 0, s, t, freqs, phases, transform,
                        n, c, c_p, size, sampling_rate, bandwidth, (float*)x_out);
   else if (dtype == IC2_BF16)
-    hipLaunchKernelGGL(synth_input_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, t, freqs, phases, transform,
+    hipLaunchKernelGGL(synth_input_kernel<bf16_t>, dim3((unsigned)(n * size)), dim3(256), 0, s, t, freqs, phases, transform,
                        n, c, c_p, size, sampling_rate, bandwidth, (bf16_t*)x_out);
   else
     IC2_CHECK_ARG(false, "synth_input_features: bad dtype %d", dtype);
