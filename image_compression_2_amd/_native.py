@@ -57,9 +57,12 @@ _SIGS = {
     "ic2_uint8_sse_scratch_doubles": [_I64],
     "ic2_uint8_sse": [_P, _P, _I64, _I64, _P, _P, _P],
     "ic2_resize_bilinear": [_P, _P, _I64, _I, _I, _I, _I, _P],
+    "ic2_rc_bound": [_I64, _I64],
+    "ic2_rc_encode": [_P, _I64, _I, _I, _I, _P, _I64, _P, _I],
+    "ic2_rc_decode": [_P, _P, _I64, _I, _I, _I, _P, _I],
 }
 _RESTYPE = {"ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
-            "ic2_uint8_sse_scratch_doubles": _I64}
+            "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64}
 
 _lib = None
 _lock = threading.Lock()

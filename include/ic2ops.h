@@ -197,6 +197,19 @@ int ic2_uint8_sse(const float* a, const float* b, int64_t n_img, int64_t per_img
  * (stylegan3_hvae_full.py:277-279), NCHW f32. */
 int ic2_resize_bilinear(const float* x, float* y, int64_t nc, int h, int w, int oh, int ow, void* stream);
 
+/* ---- entropy coding of the codebook indices (HOST pointers; no GPU) ----------------------------------------
+ * Replaces the reference's CABAC stage (cabac_compression.py:60-406: ContextModel, ArithmeticCoder,
+ * cabac_encode / cabac_decode; non-functional there) with a context-adaptive binary range coder:
+ * bit-tree binarisation, contexts = (previous symbol in the w vector, same position in the previous w vector).
+ * codes: int32 [n_streams][num_ws][w_dim], each in [0, n_symbols); one independent byte stream per image,
+ * concatenated into out; stream_bytes[n_streams] receives the sizes.  n_threads <= 0: hardware concurrency
+ * (capped at 16).  ic2_rc_bound gives a sufficient out_cap. */
+int64_t ic2_rc_bound(int64_t n_streams, int64_t per_stream);
+int ic2_rc_encode(const int32_t* codes, int64_t n_streams, int num_ws, int w_dim, int n_symbols, uint8_t* out,
+                  int64_t out_cap, int64_t* stream_bytes, int n_threads);
+int ic2_rc_decode(const uint8_t* in, const int64_t* stream_bytes, int64_t n_streams, int num_ws, int w_dim,
+                  int n_symbols, int32_t* codes_out, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

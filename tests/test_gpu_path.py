@@ -264,3 +264,29 @@ def test_psnr_of_path_matches_oracle_metric(cuda, gen256):
     img = gen256.synthesis(ws)
     x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(cuda)
     assert icm.psnr(img, x) == pytest.approx(om.psnr(img.cpu(), x.cpu()), abs=1e-9)
+
+
+# ------------------------------------------------------------------ entropy-coded codebook container
+def test_cabac_compressor_round_trip(cuda, gen256, tmp_path):
+    """CABACCompressor (ref cabac_compression.py:409-588, whose coder cannot run): the entropy-coded codes
+    decode to exactly the codebook indices of GumbelSoftmaxCompressor.compress, the image equals its
+    decompress, and the .cabac file round-trips."""
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024).to(cuda).eval()
+    comp = ic2.CABACCompressor(enc, gen256)
+    gcomp = ic2.GumbelSoftmaxCompressor(enc, gen256)
+    x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(21)) * 2 - 1).to(cuda)
+    torch.manual_seed(3)
+    blob, meta = comp.compress(x)
+    torch.manual_seed(3)
+    codes = gcomp.compress(x)
+    assert tuple(meta["shape"]) == (2, 16, 512) and meta["use_cabac"]
+    dec = ic2.cabac_decode(blob, comp.context_model, meta["shape"])
+    assert np.array_equal(dec, codes.numpy().astype(np.int32))
+    img = comp.decompress(blob, meta)
+    assert torch.equal(img, gcomp.decompress(codes))
+    f = str(tmp_path / "img.cabac")
+    torch.manual_seed(3)
+    orig, comp_size, ratio = comp.save_compressed(x, f)
+    img2, ratio2 = comp.load_compressed(f)
+    assert torch.equal(img2, img) and ratio2 == ratio and comp_size == len(blob)
