@@ -274,7 +274,7 @@ def test_cabac_compressor_round_trip(cuda, gen256, tmp_path):
     torch.manual_seed(0)
     enc = ic2.HVAE_VGG_Encoder(img_resolution=1024).to(cuda).eval()
     comp = ic2.CABACCompressor(enc, gen256)
-    gcomp = ic2.GumbelSoftmaxCompressor(enc, gen256)
+    gcomp = ic2.GumbelSoftmaxCompressor(enc, gen256).to(cuda)
     x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(21)) * 2 - 1).to(cuda)
     torch.manual_seed(3)
     blob, meta = comp.compress(x)
