@@ -133,13 +133,15 @@ extern "C" int ic2_fm_debug_fetch(uint32_t* host, int which) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fm_dbg), 8192 * 4, (size_t)which * 8192 * 4, hipMemcpyDeviceToHost);
 }
 #define FM_DUMP(which, ptr, ndw) \
-  if (blockIdx.x == 0) for (int i_ = tid; i_ < (ndw); i_ += 256) g_fm_dbg[which][i_] = (ptr)[i_];
+  if (blockIdx.x == 0) for (int i_ = tid; i_ < (ndw); i_ += (int)blockDim.x) g_fm_dbg[which][i_] = (ptr)[i_];
 #else
 #define FM_DUMP(which, ptr, ndw) (void)0
 #endif
 
-template <int U, int DELTA, bool IN_F16, bool ALIAS>
-__global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles) {
+template <int U, int DELTA, bool IN_F16, bool ALIAS, int NW>
+__global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int ntiles) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NT = 64 * NW, RR = 16 / NW;  // threads; grid rows (and output columns) per wave per block
   using G = FmGeom<U>;
   constexpr int NIN = G::NIN, NCH = NIN * NIN * 2;  // input pixels x 16-B halves
   __shared__ __attribute__((aligned(16))) uint32_t lds[ALIAS ? G::LDS_DW_ALIAS : G::LDS_DW];
@@ -158,7 +160,7 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
   // tap tables with zero guard bands, so every per-lane filter-matrix entry below is a branch-free read
   // (tap ranges: up [-43, 63], down [-30, 47]): gu at [48, 72) of [0, 116), gd at [148, 160) of [116, 196),
   // gdg (gain folded) at [228, 240) of [196, 276)
-  for (int i = tid; i < FM_TAPS; i += 256) {
+  for (int i = tid; i < FM_TAPS; i += NT) {
     float v = 0.f;
     if (i >= 48 && i < 72) v = a.gu[i - 48];
     else if (i >= 148 && i < 160) v = a.gd[i - 148];
@@ -197,19 +199,19 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
     tile_geom(t, n, oy0, ox0, c0);
     const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
     if constexpr (IN_F16) {
-      for (int k = wave; k * 64 < NCH; k += 4)
+      for (int k = wave; k * 64 < NCH; k += NW)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)chunk_src(k * 64 + lane, n, sy0,
                                                                                                    sx0, c0),
                                          (__attribute__((address_space(3))) void*)(in_img + k * 256), 16, 0, 0);
     } else {
-      constexpr int PER = (NCH + 255) / 256;
+      constexpr int PER = (NCH + NT - 1) / NT;
       uint4 v[PER];
 #pragma unroll
       for (int r = 0; r < PER; ++r)  // every load in flight before the first conversion
-        v[r] = *reinterpret_cast<const uint4*>(chunk_src(tid + 256 * r, n, sy0, sx0, c0));
+        v[r] = *reinterpret_cast<const uint4*>(chunk_src(tid + NT * r, n, sy0, sx0, c0));
 #pragma unroll
       for (int r = 0; r < PER; ++r) {
-        const int e = tid + 256 * r;
+        const int e = tid + NT * r;
         if (e < NCH)
           *reinterpret_cast<uint4*>(in_img + e * 4) =
               make_uint4(fm_bf2_to_h2(v[r].x), fm_bf2_to_h2(v[r].y), fm_bf2_to_h2(v[r].z), fm_bf2_to_h2(v[r].w));
@@ -269,9 +271,9 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
     __syncthreads();                                   // everyone's; and the previous tile fully consumed
     FM_DUMP(0, in_img, G::IN_DW);
 
-    fm_f4 acc[4];
+    fm_f4 acc[RR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = fm_f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < RR; ++i) acc[i] = fm_f4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
     for (int b = 0; b < G::NB; ++b) {
@@ -280,13 +282,13 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
       // as groups (every column's LDS read, then every MFMA, then every store) with scheduling barriers
       // between them, so the columns' LDS and MFMA latencies overlap instead of forming one serial chain
       {
-        constexpr int NC = (NIN + 3) / 4;
+        constexpr int NC = (NIN + NW - 1) / NW;
         const int w0 = fm_win<U, DELTA, NIN>(16 * b);
         fm_s4 xa[NC];
         fm_f4 vt[NC];
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-          const int x = min(wave + 4 * i, NIN - 1);
+          const int x = min(wave + NW * i, NIN - 1);
           xa[i] = fm_tr_read(in_img + (w0 + 4 * g + tq) * G::IN_PITCH + x * 8 + 2 * tp);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -302,7 +304,7 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
         }
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-          const int x = min(wave + 4 * i, NIN - 1);
+          const int x = min(wave + NW * i, NIN - 1);
           FM_SETTLE(vt[i]);
           *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) =
               fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
@@ -317,26 +319,26 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
       // MFMA chains interleave)
       // grouped like the vertical pass: all 12 LDS reads, all 12 up MFMAs, the activations, the 8 down
       // MFMAs, the stores
-      fm_s4 vb[4][G::NB];
+      fm_s4 vb[RR][G::NB];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+      for (int rr = 0; rr < RR; ++rr)
 #pragma unroll
         for (int tt = 0; tt < G::NB; ++tt) {
           const int w0 = fm_win<U, DELTA, NIN>(16 * tt);
-          vb[rr][tt] = fm_tr_read(v_img + (wave + 4 * rr) * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
+          vb[rr][tt] = fm_tr_read(v_img + (wave + NW * rr) * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
         }
       __builtin_amdgcn_sched_barrier(0);
-      fm_f4 u[4][G::NB];
+      fm_f4 u[RR][G::NB];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+      for (int rr = 0; rr < RR; ++rr)
 #pragma unroll
         for (int tt = 0; tt < G::NB; ++tt)
           u[rr][tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmat[tt], __builtin_bit_cast(fm_h4, vb[rr][tt]),
                                                             fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      fm_h4 au[4][G::NB];
+      fm_h4 au[RR][G::NB];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+      for (int rr = 0; rr < RR; ++rr)
 #pragma unroll
         for (int tt = 0; tt < G::NB; ++tt) {
           FM_SETTLE(u[rr][tt]);
@@ -350,37 +352,37 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
 #endif
         }
       __builtin_amdgcn_sched_barrier(0);
-      fm_f4 d[4];
+      fm_f4 d[RR];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
+      for (int rr = 0; rr < RR; ++rr) {
         const uint2 a0 = __builtin_bit_cast(uint2, au[rr][0]), a1 = __builtin_bit_cast(uint2, au[rr][1]);
         d[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a0, a1), gdh01, fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
       // block 2 as a second 16x16x32 with a zero upper half: a 16x16x16 accumulating onto the 16x16x32's
       // result one instruction later reads stale rows 0-1 of the accumulator (mixed-shape srcC hazard)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
+      for (int rr = 0; rr < RR; ++rr) {
         const uint2 a2 = __builtin_bit_cast(uint2, au[rr][2]);
         d[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(a2, make_uint2(0u, 0u)), gdh2, d[rr], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (ALIAS) __syncthreads();  // D overwrites V: every wave's horizontal reads are done
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
+      for (int rr = 0; rr < RR; ++rr) {
         FM_SETTLE(d[rr]);
-        *reinterpret_cast<uint2*>(d_img + (wave + 4 * rr) * G::D_PITCH + li * G::D_XP + 2 * g) =
+        *reinterpret_cast<uint2*>(d_img + (wave + NW * rr) * G::D_PITCH + li * G::D_XP + 2 * g) =
             fm_pack4(d[rr][0], d[rr][1], d[rr][2], d[rr][3]);
       }
       __syncthreads();
       if (b == 0) FM_DUMP(2, d_img, G::D_DW);
       // ---- vertical down: accumulate block b's 16 grid rows into this wave's 4 output columns
-      fm_s4 da[4];
+      fm_s4 da[RR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + 4 * i) * G::D_XP + 2 * tp);
+      for (int i = 0; i < RR; ++i)
+        da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + NW * i) * G::D_XP + 2 * tp);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < RR; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[b], acc[i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -393,8 +395,8 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
     }
     const int gy = oy0 + li;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int gx = ox0 + wave + 4 * i;
+    for (int i = 0; i < RR; ++i) {
+      const int gx = ox0 + wave + NW * i;
       if (gy < a.out_h && gx < a.out_w) {
         const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
                                    (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
@@ -404,7 +406,7 @@ __global__ void __launch_bounds__(256) flrelu_mfma_kernel(FlrArgs a, int ntiles)
   }
 }
 
-template <int U, int DELTA, bool IN_F16, bool ALIAS>
+template <int U, int DELTA, bool IN_F16, bool ALIAS, int NW>
 static void fm_launch_alias(const FlrArgs& a, int ntiles, hipStream_t s) {
   // persistent grid: every CU filled to the kernel's occupancy, capped by the tile count
   static int resident = 0;
@@ -412,11 +414,13 @@ static void fm_launch_alias(const FlrArgs& a, int ntiles, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS, NW>, 64 * NW,
+                                                       0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS>), dim3((unsigned)grid), dim3(256), 0, s, a, ntiles);
+  hipLaunchKernelGGL((flrelu_mfma_kernel<U, DELTA, IN_F16, ALIAS, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a,
+                     ntiles);
 }
 
 // IC2_FLR_ALIAS=0/1 selects the separate-V/D (3 workgroups per CU, default) or the aliased (4 per CU) LDS
@@ -429,8 +433,16 @@ static void fm_launch_one(const FlrArgs& a, int ntiles, hipStream_t s) {
     const char* e = getenv("IC2_FLR_ALIAS");
     return e ? atoi(e) : 0;
   }();
-  if (U == 2 && alias) fm_launch_alias<U, DELTA, IN_F16, true>(a, ntiles, s);
-  else fm_launch_alias<U, DELTA, IN_F16, false>(a, ntiles, s);
+  // IC2_FLR_WAVES=8: the same tile on 8 waves (half the rows / columns per wave, 90 VGPRs, 2 workgroups =
+  // 16 waves per CU instead of 12).  Measured slower (FLR 9.0 vs 8.1 ms per C2 step): the kernel wants
+  // independent MFMA chains per wave between barriers more than it wants waves.
+  static const int waves = [] {
+    const char* e = getenv("IC2_FLR_WAVES");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
+  if (U == 2 && alias) fm_launch_alias<U, DELTA, IN_F16, true, 4>(a, ntiles, s);
+  else if (waves == 8) fm_launch_alias<U, DELTA, IN_F16, false, 8>(a, ntiles, s);
+  else fm_launch_alias<U, DELTA, IN_F16, false, 4>(a, ntiles, s);
 }
 
 template <bool IN_F16>

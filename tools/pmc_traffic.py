@@ -6,8 +6,9 @@ Units and gfx950 corrections (MI355X_MICROARCH.md, "HBM"; cdna_hip_programming.m
 FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE reports exactly half the bytes of a wide coalesced
 streaming read on gfx950 (the igemm operand loads are 16-B-per-lane LDS-DMA), so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
-Per launch = the bytes of every igemm* dispatch (the split-K combine included) / the number of
-ic2_conv_igemm calls (= GEMM-body dispatches), matching how bench.py times the kernel.
+Per launch = the bytes of every dispatch behind ic2_conv_igemm (igemm*, the split-K combine, the halo conv
+and the ToRGB kernel) / the number of ic2_conv_igemm calls (= conv-body dispatches), matching how bench.py
+times the kernel.
 """
 import collections
 import csv
@@ -25,7 +26,7 @@ def main():
         for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"]
-                if "igemm" not in k:
+                if not any(t in k for t in ("igemm", "hconv_kernel", "torgb_kernel")):
                     continue
                 c = r["Counter_Name"]
                 per[c] += float(r["Counter_Value"])
