@@ -7,7 +7,8 @@ pickle stores every network as a ``torch_utils.persistence`` record: ``_reconstr
 ``pickle.load`` would ``exec``.  Here that source is never run:
 
 * ``find_class`` resolves only a fixed allow-list (the persistence reconstructor, tensor / parameter / storage
-  rebuilders, ``collections.OrderedDict``, torch dtypes, ``dnnlib.EasyDict``); every other global becomes an inert
+  rebuilders, ``collections.OrderedDict``, torch dtypes, ``dnnlib.EasyDict``, numpy's scalar / array
+  reconstructors); every other global becomes an inert
   placeholder whose construction records its arguments and runs nothing;
 * storages are decoded with ``torch.load(..., weights_only=True)`` instead of torch's ``_load_from_bytes``
   (which uses ``weights_only=False``);
@@ -28,7 +29,13 @@ import collections
 import io
 import pickle
 
+import numpy as np
 import torch
+
+try:  # numpy >= 2 keeps the reconstructors in numpy._core (numpy.core is a deprecated alias)
+    from numpy._core import multiarray as _np_ma
+except ImportError:  # pragma: no cover - numpy 1.x
+    from numpy.core import multiarray as _np_ma
 
 __all__ = ["PersistentRecord", "SafeUnpickler", "load_network_pkl", "record_state_dict", "generator_from_record"]
 
@@ -121,6 +128,13 @@ _ALLOWED = {
     ("builtins", "frozenset"): frozenset,
     ("builtins", "slice"): slice,
     ("torch", "Size"): torch.Size,
+    # SG3 layers keep numpy scalars / arrays as attributes (sizes, sampling rates): data-only constructors
+    ("numpy", "dtype"): np.dtype,
+    ("numpy", "ndarray"): np.ndarray,
+    ("numpy.core.multiarray", "scalar"): _np_ma.scalar,
+    ("numpy._core.multiarray", "scalar"): _np_ma.scalar,
+    ("numpy.core.multiarray", "_reconstruct"): _np_ma._reconstruct,
+    ("numpy._core.multiarray", "_reconstruct"): _np_ma._reconstruct,
 }
 _DTYPES = {n for n in dir(torch) if isinstance(getattr(torch, n, None), torch.dtype)}
 

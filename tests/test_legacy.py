@@ -153,3 +153,33 @@ def test_missing_or_extra_tensors_fail_strictly():
             sys.modules.pop(k, None) if v is None else sys.modules.__setitem__(k, v)
     with pytest.raises(RuntimeError, match="w_avg"):
         legacy.load_network_pkl(io.BytesIO(blob), device="cpu")
+
+
+def test_easydict_kwargs_as_written_by_sg3_train():
+    """SG3's train.py passes mapping_kwargs as a dnnlib.EasyDict; the loader maps that class to a plain dict."""
+    mod = types.ModuleType("dnnlib.util")
+
+    class EasyDict(dict):
+        pass
+    EasyDict.__module__ = "dnnlib.util"
+    EasyDict.__qualname__ = "EasyDict"
+    mod.EasyDict = EasyDict
+    pkg = types.ModuleType("dnnlib")
+    pkg.util = mod
+    saved = {k: sys.modules.get(k) for k in ("dnnlib", "dnnlib.util")}
+    sys.modules.update({"dnnlib": pkg, "dnnlib.util": mod})
+    try:
+        torch.manual_seed(4)
+        G = Generator(img_resolution=256)
+        kw = _sg3_kwargs(256)
+        kw["mapping_kwargs"] = EasyDict(num_layers=2)
+        blob = _write_pkl(G, kw)
+    finally:
+        for k, v in saved.items():
+            sys.modules.pop(k, None) if v is None else sys.modules.__setitem__(k, v)
+    up = legacy.SafeUnpickler(io.BytesIO(blob))
+    rec = up.load()["G_ema"]
+    assert not up.opaque
+    assert rec.init_kwargs["mapping_kwargs"]["num_layers"] == 2
+    G2 = legacy.generator_from_record(rec, device="cpu")
+    assert all(torch.equal(a, b) for a, b in zip(G.state_dict().values(), G2.state_dict().values()))
