@@ -1,19 +1,32 @@
 """Benchmark of the encode -> 8-bit quantize -> synthesize path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--batch B] [--precision bf16|fp32]
+                    [--no-roofline] [--cpu-baseline-images M] [--dry-run]
 
 A step = one pass of the hot path over one synthetic batch already resident in HBM:
 HVAE_VGG_Encoder(img_resolution=1024) on 256^2 images -> 8-bit uniform quantizer (deterministic, means)
 -> StyleGAN3-T synthesis -> uint8 PSNR sums vs the input -> all_reduce(SUM) of the fp64 metric record.
-Random-init weights of the named architectures (no checkpoints offline), seeded synthetic inputs.
-For N > 1 (torchrun, one process per GPU, RCCL) every rank runs its own batch: weak scaling.
-Prints ONE JSON line (rank 0).
+Random-init weights of the named architectures (no checkpoints offline), seeded synthetic inputs
+(seed 1000 + rank).
+
+Multi-GPU: one process per GPU, batch-sharded, weak scaling (every rank runs its own batch).  Under torchrun
+the ranks come from the env; `python bench.py --gpus N` without torchrun spawns the N ranks itself
+(distributed.launch: the parent never touches the GPU).  `--dry-run` runs the same launcher, rank seeding,
+barrier / max-over-ranks timing and reductions on the CPU over gloo with a stand-in step (tests).
+
+Timing protocol: W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier +
+synchronize on both sides; value = images of all ranks / the max over ranks of that wall time.  Each timed
+step is also bracketed by HIP events on the launching stream (torch's current stream, which every libic2ops
+kernel is enqueued on): ms_per_step_median.  The per-kernel roofline timers run in a SEPARATE instrumented
+pass after the headline loop, so the headline number carries no instrumentation.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -21,6 +34,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+from image_compression_2_amd import distributed as icd  # noqa: E402  (no GPU access at import)
 
 CONFIGS = {
     # name: (input res, generator res, per-GPU batch, description)
@@ -32,48 +47,58 @@ F32_PEAK_TFLOPS = 157.3     # f32 MFMA / VALU
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline-images", type=int, default=3, help="0 disables the CPU baseline leg")
     ap.add_argument("--no-roofline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="CPU / gloo rehearsal of launcher + timing + reductions")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file (rank 0)")
+    return ap.parse_args(argv)
 
 
-class IgemmTimer:
-    """Wraps every ic2_conv_igemm[_ws] call (the dominant kernel, plus its split-K combine where the launch
-    plan splits K: all encoder convs, the synthesis input 1x1 and every modulated conv) with HIP events on
-    the launching stream -- torch's current stream, which is the stream every libic2ops kernel is enqueued on."""
+# ------------------------------------------------------------------------------------------------
+# instrumentation (separate pass)
+class CallTimer:
+    """Brackets every libic2ops call whose name is in `names` with HIP events on the launching stream
+    (torch's current stream: every libic2ops kernel is enqueued there)."""
 
-    def __init__(self, nv):
+    def __init__(self, nv, names):
         self.nv = nv
-        self.orig = nv.call
-        self.events = []
+        self.names = set(names)
+        self.events = {n: [] for n in names}
         self.enabled = False
+        self._orig = None
 
     def install(self):
-        timer = self
+        timer, orig = self, self.nv.call
+        self._orig = orig
 
         def call(name, *args):
-            if not timer.enabled or name not in ("ic2_conv_igemm", "ic2_conv_igemm_ws"):
-                return timer.orig(name, *args)
+            if not timer.enabled or name not in timer.names:
+                return orig(name, *args)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            rc = timer.orig(name, *args)
+            rc = orig(name, *args)
             e.record()
-            timer.events.append((s, e))
+            timer.events[name].append((s, e))
             return rc
 
         self.nv.call = call
 
-    def result(self):
+    def uninstall(self):
+        if self._orig is not None:
+            self.nv.call = self._orig
+
+    def total(self, names):
         torch.cuda.synchronize()
-        return sum(s.elapsed_time(e) for s, e in self.events), len(self.events)
+        ev = [p for n in names for p in self.events[n]]
+        return sum(s.elapsed_time(e) for s, e in ev), len(ev)
 
 
 def algorithmic_flops_per_image(enc, G, res):
@@ -97,9 +122,9 @@ def algorithmic_flops_per_image(enc, G, res):
 
 
 def algorithmic_bytes_per_image(enc, G, res, esz):
-    """Compulsory HBM bytes of the igemm launches per image: each conv reads its input activation and
-    writes its output once (padded channel strides, esz bytes each; ToRGB writes 3 f32 channels).
-    Weights are per launch, not per image, and are added by the caller."""
+    """Compulsory HBM bytes of the conv launches per image: each conv reads its input activation and writes
+    its output once (padded channel strides, esz bytes each; ToRGB writes 3 f32 channels).  Weights are per
+    launch, not per image, and are added by the caller."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
     total, h = 0.0, res
     total += h * h * (p32(enc.from_rgb.in_channels) + p32(enc.from_rgb.out_channels)) * esz
@@ -120,7 +145,7 @@ def algorithmic_bytes_per_image(enc, G, res, esz):
 
 
 def weight_bytes(enc, G, res, esz):
-    """Packed weight bytes of the convs one step runs, and their count (= igemm calls per step)."""
+    """Packed weight bytes of the convs one step runs, and their count (= conv calls per step)."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
     convs, h = [enc.from_rgb], res
     for blk in enc.blocks:
@@ -135,8 +160,31 @@ def weight_bytes(enc, G, res, esz):
     return tot, len(convs) + 1 + len(list(G.synthesis.layers()))
 
 
+def flr_work_per_image(G):
+    """Filtered-lrelu algorithmic work per image: polyphase separable FIR FLOPs
+    (vertical up: U1 x S_conv outputs x taps_u/up, horizontal up: U1 x U1 x taps_u/up, horizontal down:
+    U1 x S_out x taps_d, vertical down: S_out^2 x taps_d; 2 FLOP per tap) x channels, and the fused kernel's
+    compulsory bytes (conv output in, 2 B, + layer output, 2 B, unpadded channels).  -> (flops, bytes, bound_s)
+    with bound_s = sum over layers of max(FIR / 157.3 TF, bytes / 8 TB/s)."""
+    flops = byts = bound = 0.0
+    for L in G.synthesis.layers():
+        if L.is_torgb:
+            continue
+        c = L.out_channels
+        s_conv = int(L.in_size[0]) + L.conv_kernel - 1
+        s_out = int(L.out_size[0])
+        up, tu, td = L.up_factor, L.up_taps, L.down_taps
+        u1 = (s_out - 1) * L.down_factor + td  # lrelu-grid side that feeds the outputs
+        f = 2 * c * (u1 * s_conv * tu / up + u1 * u1 * tu / up + u1 * s_out * td + s_out * s_out * td)
+        b = c * (s_conv * s_conv + s_out * s_out) * 2
+        flops += f
+        byts += b
+        bound += max(f / (F32_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9))
+    return flops, byts, bound
+
+
 def pmc_traffic(config, precision, batch):
-    """roofline.traffic: HBM bytes per igemm launch from the committed PMC run for this exact workload
+    """roofline.traffic: HBM bytes per conv launch from the newest committed PMC run for this exact workload
     (tools/pmc_traffic.sh; FETCH_SIZE x2 + WRITE_SIZE, KiB -> bytes), or None when there is none."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_traffic_{config}_{precision}_b{batch}.json")))
@@ -146,8 +194,20 @@ def pmc_traffic(config, precision, batch):
     return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(res, gen_res, n_images):
-    """The oracle (pure-PyTorch fp32 CPU restatement) timed on the host cores: encode + quantize + decode."""
+    """The oracle (pure-PyTorch fp32 CPU restatement) timed on the host cores: encode + quantize + decode of
+    n_images, the fine fc1 drawn exactly as the reference re-creates it (nn.Linear(128, 256) default init,
+    stylegan3_hvae_full.py:225-230)."""
     from oracle import encoder as oe
     from oracle import sg3
     import image_compression_2_amd as ic2
@@ -156,7 +216,9 @@ def cpu_baseline(res, gen_res, n_images):
     sd_e = {k: v.detach() for k, v in enc.state_dict().items()}
     sd_g = sg3.init_params(gen_res, seed=1)
     x = torch.rand(n_images, 3, res, res, generator=torch.Generator().manual_seed(1000)) * 2 - 1
-    fc1 = (torch.randn(256, 128) * 0.05, torch.zeros(256))
+    torch.manual_seed(5)
+    lin = torch.nn.Linear(128, 256)
+    fc1 = (lin.weight.detach(), lin.bias.detach())
     t0 = time.perf_counter()
     with torch.no_grad():
         _, m, _ = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
@@ -164,67 +226,101 @@ def cpu_baseline(res, gen_res, n_images):
         sg3.synthesis_forward(sd_g, gen_res, q)
     dt = time.perf_counter() - t0
     return dict(value=round(n_images / dt, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
+                cpu_model=cpu_model(),
                 sample=f"{n_images} image(s) {res}x{res}, encoder(1024-config) + 8-bit quantize + SG3-T-{gen_res} "
-                       f"synthesis, fp32, oracle/ restatement, {dt:.1f} s")
+                       f"synthesis, fp32, oracle/ restatement on {torch.get_num_threads()} threads, {dt:.1f} s; "
+                       f"B=1 / B=32 / 1024^2 rows: profiles/r2_cpu_baseline.json")
 
 
-def main():
-    args = parse()
-    from image_compression_2_amd import distributed as icd
-    rank, world, local = icd.init()
-    assert world == args.gpus or (world == 1 and args.gpus == 1), \
-        f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)"
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    import image_compression_2_amd as ic2
-    from image_compression_2_amd import _native as nv
-    from image_compression_2_amd import metrics as icm
+# ------------------------------------------------------------------------------------------------
+def timed_loop(step, steps, sync, barrier, use_events):
+    """Barrier + sync, EXACTLY `steps` steps, sync + barrier + sync.  -> (last output, wall s, per-step ms)."""
+    sync()
+    barrier()
+    sync()
+    marks = []
+    out = None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if use_events:
+            s = torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = step()
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            marks.append((s, e))
+        else:
+            ts = time.perf_counter()
+            out = step()
+            marks.append(time.perf_counter() - ts)
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    per = [s.elapsed_time(e) for s, e in marks] if use_events else [m * 1e3 for m in marks]
+    return out, elapsed, per
 
+
+def run(args):
+    dry = args.dry_run
+    rank, world, local = icd.init("gloo" if dry else None)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     res, gen_res, batch, desc = CONFIGS[args.config]
     batch = args.batch or batch
-    torch.manual_seed(0)
-    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=args.precision).to(dev).eval()
-    torch.manual_seed(1)
-    G = ic2.Generator(img_resolution=gen_res, precision=args.precision).to(dev).eval()
-    comp = ic2.StyleGAN3Compressor(enc, G)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x = torch.rand(batch, 3, res, res, generator=g, device=dev) * 2 - 1
+    if dry:
+        dev = torch.device("cpu")
+        sync = lambda: None
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        sync = torch.cuda.synchronize
+    barrier = lambda: icd.barrier(dev)
 
-    timer = IgemmTimer(nv)
-    timer.install()
+    if dry:
+        # stand-in step: the same seeded per-rank batch, a metric record and its all_reduce
+        g = torch.Generator().manual_seed(1000 + rank)
+        x = torch.rand(batch, 3, 16, 16, generator=g) * 2 - 1
+        from oracle import metrics as om
 
-    def step():
-        with torch.no_grad():
-            q = comp.compress(x, quantization_bits=8, deterministic=True)
-            img = comp.decompress(q)
-            sse = icm.uint8_sse(img, x)
-        vec = torch.stack([sse.sum(), torch.tensor(float(img.numel()), device=dev, dtype=torch.float64),
-                           torch.tensor(float(batch), device=dev, dtype=torch.float64)])
-        return icd.allreduce_sum(vec, device=dev)
+        def step():
+            sse = float(om.sse_uint8(x, x.flip(0)).sum())
+            vec = torch.tensor([sse, float(x.numel()), float(batch)], dtype=torch.float64)
+            return icd.allreduce_sum(vec)
+        enc = G = comp = nv = None
+    else:
+        import image_compression_2_amd as ic2
+        from image_compression_2_amd import _native as nv
+        from image_compression_2_amd import metrics as icm
+        torch.manual_seed(0)
+        enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=args.precision).to(dev).eval().requires_grad_(False)
+        torch.manual_seed(1)
+        G = ic2.Generator(img_resolution=gen_res, precision=args.precision).to(dev).eval()
+        comp = ic2.StyleGAN3Compressor(enc, G)
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        x = torch.rand(batch, 3, res, res, generator=g, device=dev) * 2 - 1
+
+        def step():
+            with torch.no_grad():
+                q = comp.compress(x, quantization_bits=8, deterministic=True)
+                img = comp.decompress(q)
+                sse = icm.uint8_sse(img, x)
+            vec = torch.stack([sse.sum(), torch.tensor(float(img.numel()), device=dev, dtype=torch.float64),
+                               torch.tensor(float(batch), device=dev, dtype=torch.float64)])
+            return icd.allreduce_sum(vec, device=dev)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    icd.barrier(dev)
-    torch.cuda.synchronize()
-    timer.enabled = not args.no_roofline
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        vec = step()
-    torch.cuda.synchronize()
-    icd.barrier(dev)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    timer.enabled = False
-    elapsed = icd.allreduce_max(elapsed, device=dev)
-    igemm_ms, n_launch = timer.result()
+    vec, elapsed, per_step = timed_loop(step, args.steps, sync, barrier, use_events=not dry)
+    elapsed_max = icd.allreduce_max(elapsed, device=dev)
+    per_rank_ms = [round(t / args.steps * 1e3, 3) for t in icd.allgather_floats(elapsed, device=dev)]
+    median_ms = statistics.median(per_step)
+    median_max = icd.allreduce_max(median_ms, device=dev)
+    checksum = icd.allgather_floats(float(x.double().sum()), device=dev)
 
     total_images = batch * args.steps * world
-    value = total_images / elapsed
+    value = total_images / elapsed_max
     vec = vec.cpu()
-    psnr = icm.psnr_from_sums(vec[0].item(), vec[1].item())
-    flops_img = algorithmic_flops_per_image(enc, G, res)
-    peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
     out = {
         "metric": "images/sec encode+decode 256px" if args.config == "c2" else "images/sec encode+decode 1024px",
         "value": round(value, 3),
@@ -232,38 +328,87 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic (seeded uniform [-1,1] images resident in HBM; random-init encoder + SG3-T weights)",
+        "data": "synthetic (seeded uniform [-1,1] images resident in HBM, seed 1000+rank; random-init encoder + "
+                "SG3-T weights)",
         "config": {"workload": desc, "global_batch": batch * world, "per_gpu_batch": batch, "resolution": res,
                    "generator": f"stylegan3-t-{gen_res} (random init)", "encoder": "HVAE_VGG_Encoder(img_resolution=1024)",
                    "quantization_bits": 8, "parallelism": f"dp{world} (batch-sharded, RCCL metric all_reduce)"},
-        "psnr_db_vs_input": round(psnr, 4),
+        "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
+        "ms_per_step_median": round(median_max, 3),
+        "per_rank_ms_per_step": per_rank_ms,
+        "rank_input_checksums": [round(c, 6) for c in checksum],
     }
-    if not args.no_roofline and igemm_ms > 0:
-        per_launch_ms = igemm_ms / n_launch
+    if dry:
+        out["dry_run"] = True
+        out["psnr_db_record"] = float(10 * torch.log10(255.0 ** 2 / (vec[0] / vec[1])))
+    else:
+        from image_compression_2_amd import metrics as icm
+        out["psnr_db_vs_input"] = round(icm.psnr_from_sums(vec[0].item(), vec[1].item()), 4)
+
+    if not dry and not args.no_roofline:
+        conv_names = ("ic2_conv_igemm", "ic2_conv_igemm_ws")
+        timer = CallTimer(nv, conv_names + ("ic2_flrelu_nhwc",))
+        timer.install()
+        timer.enabled = True
+        n_inst = min(args.steps, 10)
+        timed_loop(step, n_inst, sync, barrier, use_events=True)
+        timer.enabled = False
+        timer.uninstall()
+        conv_ms, n_launch = timer.total(conv_names)
+        flr_ms, n_flr = timer.total(("ic2_flrelu_nhwc",))
+        flops_img = algorithmic_flops_per_image(enc, G, res)
+        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
         traffic, traffic_src = pmc_traffic(args.config, args.precision, batch)
         esz = 2 if args.precision == "bf16" else 4
         wb, n_conv = weight_bytes(enc, G, res, esz)
         alg_bytes = (algorithmic_bytes_per_image(enc, G, res, esz) * batch + wb) / n_conv
-        achieved = flops_img * batch * args.steps / (igemm_ms * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": "ic2 igemm_kernel (all conv/modconv launches)",
+        achieved = flops_img * batch * n_inst / (conv_ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "ic2 conv family (igemm / halo conv / ToRGB, every "
+                                                      "encoder conv, synthesis input 1x1 and modulated conv)",
                            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                            "traffic_src": traffic_src, "algorithmic_bytes_per_launch": round(alg_bytes),
-                           "launches": n_launch, "avg_launch_ms": round(per_launch_ms, 4),
+                           "launches": n_launch, "avg_launch_ms": round(conv_ms / max(n_launch, 1), 4),
+                           "conv_ms_per_step": round(conv_ms / n_inst, 3),
                            "path_frac": round(value / world * flops_img / (peak * 1e12), 4),
                            "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}
-    if rank == 0 and world == 1 and args.cpu_baseline_images > 0:
+        if args.precision == "bf16" and n_flr:
+            f_img, b_img, bound_img = flr_work_per_image(G)
+            flr_step = flr_ms / n_inst
+            bound_step = bound_img * batch * 1e3
+            out["roofline"]["flr"] = {
+                "kernel": "ic2 flrelu_mfma (fused filtered lrelu, every synthesis layer but ToRGB)",
+                "bound": "valu (FIR on f32 VALU, SURVEY.md 8(d)); the kernel itself runs the FIR on f16 MFMA",
+                "fir_gflop_per_image": round(f_img / 1e9, 3), "bytes_per_image": round(b_img),
+                "ms_per_step": round(flr_step, 3), "bound_ms_per_step": round(bound_step, 3),
+                "frac_of_bound": round(bound_step / flr_step, 4),
+                "achieved_tflops": round(f_img * batch / (flr_step * 1e-3) / 1e12, 2),
+                "achieved_gbs": round(b_img * batch / (flr_step * 1e-3) / 1e9, 1), "launches": n_flr}
+
+    if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
         out["cpu_baseline"] = cpu_baseline(res if args.config == "c2" else 256, gen_res if args.config == "c2" else 256,
                                            args.cpu_baseline_images)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        icd.launch(args.gpus, run, args)   # self-launch: one spawned process per GPU
+        return
+    run(args)
 
 
 if __name__ == "__main__":

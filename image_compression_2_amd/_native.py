@@ -136,6 +136,26 @@ def require_gpu(*tensors):
             raise RuntimeError("expected a contiguous tensor")
 
 
+class AutogradUnsupported(RuntimeError):
+    pass
+
+
+def forbid_autograd(what, tensors=(), modules=()):
+    """The HIP forwards return tensors without a grad_fn.  Where the reference caller would train through
+    them (stylegan3_hvae_full.py:669-696: the encoder's loss backpropagates through the frozen generator into
+    W+), a silent result would run and learn nothing, so refuse instead: raise when grad mode is on and any
+    input or parameter requires grad."""
+    if not torch.is_grad_enabled():
+        return
+    need = any(t is not None and t.requires_grad for t in tensors)
+    need = need or any(p.requires_grad for m in modules for p in m.parameters())
+    if need:
+        raise AutogradUnsupported(
+            f"{what}: autograd through the HIP path is not implemented for this module (training, SURVEY.md "
+            "8(f) #3).  Run inference under torch.no_grad() / torch.inference_mode(), or freeze the module with "
+            ".requires_grad_(False)")
+
+
 def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 

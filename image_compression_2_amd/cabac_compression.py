@@ -22,10 +22,12 @@ import numpy as np
 import torch
 
 from . import _native as nv
-from .gumbel_softmax_compression import GumbelSoftmaxDiscretization, codebook_argmin, codebook_lookup
+from .gumbel_softmax_compression import GumbelSoftmaxDiscretization, check_codes, codebook_argmin, codebook_lookup
 
 _MAGIC = b"IC2R"
 _VERSION = 1
+_MAX_SYMBOLS_PER_STREAM = 1 << 24   # an untrusted header may not ask for more than this per image
+_MAX_STREAMS = 1 << 16
 
 
 class ContextModel:
@@ -74,6 +76,11 @@ def cabac_decode(encoded_bytes, context_model, shape=None):
     _, version, b, num_ws, w_dim, n_symbols = struct.unpack_from("<4s5I", buf, 0)
     if version != _VERSION:
         raise ValueError(f"unsupported IC2R version {version}")
+    # the header is untrusted: bound the allocation it asks for before making it
+    if not (0 < b <= _MAX_STREAMS and 0 < num_ws and 0 < w_dim and num_ws * w_dim <= _MAX_SYMBOLS_PER_STREAM):
+        raise ValueError(f"implausible IC2R header: {b} streams of {num_ws} x {w_dim} symbols")
+    if len(buf) < 24 + 4 * b:
+        raise ValueError("truncated IC2R header")
     if n_symbols != context_model.n_symbols:
         raise ValueError(f"stream has {n_symbols} symbols, context model {context_model.n_symbols}")
     if shape is not None and tuple(shape) != (b, num_ws, w_dim):
@@ -125,13 +132,14 @@ class CABACCompressor:
 
     def decompress(self, encoded_bytes, metadata, noise_mode="const"):
         shape = tuple(metadata["shape"])
-        if metadata["use_cabac"]:
+        if metadata.get("use_cabac", True):  # the reference's default (ref :512)
             codes = cabac_decode(encoded_bytes, self.context_model, shape)
         else:
             codes = np.frombuffer(encoded_bytes, dtype=np.int32).reshape(shape)
         with torch.no_grad():
             dev = self.discretization.codebook.device
-            w, _ = codebook_lookup(torch.from_numpy(codes.astype(np.int64)).to(dev), self.discretization.codebook)
+            w, flag = codebook_lookup(torch.from_numpy(codes.astype(np.int64)).to(dev), self.discretization.codebook)
+            check_codes(flag, self.discretization.n_embeddings)
             return self.generator.synthesis(w, noise_mode=noise_mode)
 
     def save_compressed(self, x, filename, use_cabac=True):

@@ -333,6 +333,7 @@ __global__ void __launch_bounds__(256) reparam_kernel(const float* __restrict__ 
                                                       int n, int num_ws, int w_dim, int ws_total, int ws_off,
                                                       float* __restrict__ w_out, float* __restrict__ mean_out,
                                                       float* __restrict__ logvar_out) {
+#pragma clang fp contract(off)  // mean + eps * std as two roundings, like the reference's torch ops (:243-245)
   const int64_t total = (int64_t)n * num_ws * w_dim;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int d = (int)(e % w_dim);
@@ -353,6 +354,7 @@ __global__ void __launch_bounds__(256) reparam_kernel(const float* __restrict__ 
 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int to_u8(float v) {
+#pragma clang fp contract(off)  // (x * 0.5 + 0.5) as two roundings (hvae_training.py:368-388)
   float t = v * 0.5f + 0.5f;
   t = fminf(fmaxf(t, 0.f), 1.f);
   return (int)(t * 255.f);  // truncation, as numpy astype(np.uint8) on [0, 255]

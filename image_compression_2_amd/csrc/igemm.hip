@@ -870,9 +870,11 @@ __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
   }
 }
 
-static bool torgb_eligible(int dtype, int cin_p, int cout_valid, int kh, int kw, int out_layout, int out_dtype) {
+// (the kernel maps output pixel p to input pixel p: 1x1, no padding)
+static bool torgb_eligible(int dtype, int cin_p, int cout_valid, int kh, int kw, int pad, int out_layout,
+                           int out_dtype) {
   static const bool on = !ig_env_off("IC2_TORGB");
-  return on && dtype == IC2_BF16 && kh == 1 && kw == 1 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
+  return on && dtype == IC2_BF16 && kh == 1 && kw == 1 && pad == 0 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
          out_dtype == IC2_F32 && (cin_p == 32 || cin_p == 64 || cin_p == 128);
 }
 
@@ -935,7 +937,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   hipStream_t s = as_stream(stream);
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
-  const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, out_layout, out_dtype);
+  const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype);
   if (torgb) {
     launch_torgb(a, s);
   } else if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {

@@ -60,6 +60,40 @@ def allreduce_max(value, device=None):
     return float(t.item())
 
 
+def allgather_floats(value, device=None):
+    """[value of rank 0, value of rank 1, ...] (a one-element list when not distributed)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned(local_rank, world, port, fn, args):
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    fn(*args)
+
+
+def launch(world, fn, *args):
+    """One process per GPU without torchrun: spawn `world` fresh interpreters (start method 'spawn', so no
+    child inherits a parent's GPU state and nothing exec's after a GPU call -- the parent never touches the
+    device), each with torchrun's env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT),
+    running fn(*args).  Raises if any rank fails."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned, args=(world, free_port(), fn, args), nprocs=world, join=True, start_method="spawn")
+
+
 def barrier(device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         if device is not None and device.type == "cuda":

@@ -31,6 +31,7 @@ def codebook_argmin(z, codebook, hist=False):
 
 
 def codebook_lookup(codes, codebook):
+    """codebook[codes] -> (f32 values, int32 flag); flag != 0 when some code lies outside [0, K)."""
     codes = codes.to(torch.int64).contiguous()
     nv.require_gpu(codes, codebook)
     out = torch.empty(codes.shape, dtype=torch.float32, device=codes.device)
@@ -38,6 +39,13 @@ def codebook_lookup(codes, codebook):
     nv.call("ic2_codebook_lookup", nv.ptr(codes), codes.numel(), nv.ptr(codebook), codebook.numel(), nv.ptr(out),
             nv.ptr(flag), nv.stream_of(codes))
     return out, flag
+
+
+def check_codes(flag, k):
+    """The reference's ``codebook[flat_codes]`` (gumbel_softmax_compression.py:258) raises on a code outside
+    [0, K); the lookup kernel raises the same way through its flag (one small sync on a path that syncs)."""
+    if int(flag.item()) != 0:
+        raise IndexError(f"code out of range for a codebook of {k} entries")
 
 
 class GumbelSoftmaxDiscretization(nn.Module):
@@ -71,6 +79,7 @@ class GumbelSoftmaxDiscretization(nn.Module):
         batch_size, num_ws, w_dim = z.shape
         if hard is None:
             hard = not self.training
+        nv.forbid_autograd("GumbelSoftmaxDiscretization.forward", (z, self.log_temperature))
         z = z.to(torch.float32).contiguous()
         nv.require_gpu(z)
         m = z.numel()
@@ -144,6 +153,7 @@ class GumbelSoftmaxCompressor(nn.Module):
             device = self.discretization.codebook.device
             codes = codes.to(device)
             w_discrete, flag = codebook_lookup(codes, self.discretization.codebook)
+            check_codes(flag, self.discretization.n_embeddings)
             return self.generator.synthesis(w_discrete, noise_mode=noise_mode)
 
     def save_compressed(self, x, filename, discrete_bits=8):
@@ -159,7 +169,10 @@ class GumbelSoftmaxCompressor(nn.Module):
         return orig_size, comp_size, orig_size / comp_size
 
     def load_compressed(self, filename, noise_mode="const"):
-        data = np.load(filename)
+        data = np.load(filename)  # allow_pickle=False (default): plain arrays only
+        if "n_embeddings" in data.files and int(data["n_embeddings"]) != self.discretization.n_embeddings:
+            raise ValueError(f"container was written with n_embeddings={int(data['n_embeddings'])}, this "
+                             f"compressor's codebook has {self.discretization.n_embeddings}")
         codes = torch.from_numpy(data["codes"])
         img = self.decompress(codes, noise_mode=noise_mode)
         return img, data["compression_ratio"]

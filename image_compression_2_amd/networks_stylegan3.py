@@ -62,6 +62,7 @@ class FullyConnectedLayer(torch.nn.Module):
         return out
 
     def forward(self, x):
+        nv.forbid_autograd("FullyConnectedLayer.forward", (x,), (self,))
         x = x.to(torch.float32).contiguous()
         nv.require_gpu(x)
         if self.activation not in ("linear", "lrelu"):
@@ -91,6 +92,7 @@ class MappingNetwork(torch.nn.Module):
     def forward(self, z, c=None, truncation_psi=1, truncation_cutoff=None, update_emas=False):
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
+        nv.forbid_autograd("MappingNetwork.forward", (z,), (self,))
         x = z.to(torch.float32).contiguous()
         nv.require_gpu(x)
         x = x * (x.square().mean(1, keepdim=True) + 1e-8).rsqrt()
@@ -156,6 +158,7 @@ class SynthesisInput(torch.nn.Module):
         return out
 
     def forward(self, w):
+        nv.forbid_autograd("SynthesisInput.forward", (w,), (self,))
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(w)
         n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad_synth(self.channels)
@@ -224,6 +227,8 @@ class SynthesisLayer(torch.nn.Module):
         pad_hi = pad_total - pad_lo
         self.padding = [int(pad_lo[0]), int(pad_hi[0]), int(pad_lo[1]), int(pad_hi[1])]
 
+        # filtered_lrelu gain (SG3 default sqrt(2) for the lrelu layers; ToRGB runs linear, gain 1)
+        self.act_gain = 1.0 if self.is_torgb else float(np.sqrt(2))
         # host copies of the (constant) FIR taps: the fused kernel takes them by value
         self._fu = None if self.up_filter is None else np.ascontiguousarray(self.up_filter.numpy(), np.float32)
         self._fd = None if self.down_filter is None else np.ascontiguousarray(self.down_filter.numpy(), np.float32)
@@ -312,7 +317,7 @@ class SynthesisLayer(torch.nn.Module):
                 conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
                 1 if fu is None else fu.shape[0], None if fd is None else fd.ctypes.data_as(ctypes.c_void_p),
                 1 if fd is None else fd.shape[0], None, self.up_factor, self.down_factor, px0, px1, py0, py1,
-                float(np.sqrt(2)), 0.2, clamp, 0, nv.ptr(post_scale), stream)
+                float(self.act_gain), 0.2, clamp, 0, nv.ptr(post_scale), stream)
         return out
 
     def forward(self, x, w, noise_mode="random", force_fp32=False, update_emas=False):
@@ -320,6 +325,7 @@ class SynthesisLayer(torch.nn.Module):
         assert noise_mode in ("random", "const", "none")
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
+        nv.forbid_autograd("SynthesisLayer.forward", (x, w), (self,))
         x = x.to(torch.float32).contiguous()
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(x, w)
@@ -420,6 +426,7 @@ class SynthesisNetwork(torch.nn.Module):
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
         assert ws.ndim == 3 and ws.shape[1] == self.num_ws and ws.shape[2] == self.w_dim, ws.shape
+        nv.forbid_autograd("SynthesisNetwork.forward", (ws,), (self,))
         ws = ws.to(torch.float32).contiguous()
         nv.require_gpu(ws)
         dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)

@@ -177,6 +177,7 @@ class HVAE_VGG_Encoder(nn.Module):
 
     def forward(self, x):
         """x [N, C, H, W] f32 in [-1, 1] -> (w_plus, means, logvars), each [N, num_ws, w_dim] f32."""
+        nv.forbid_autograd("HVAE_VGG_Encoder.forward", (x,), (self,))
         x = _check_input(x)
         dt = nv.torch_dtype(self.precision)
         stream = nv.stream_of(x)
@@ -211,6 +212,7 @@ class VGGBlock(nn.Module):
         return _group_norm_lrelu(self.norm2, y, pool, dt, stream)
 
     def forward(self, x):
+        nv.forbid_autograd("VGGBlock.forward", (x,), (self,))
         x = _check_input(x)
         stream = nv.stream_of(x)
         return _to_nchw(self.run_nhwc(_to_nhwc(x, torch.float32, stream), torch.float32, self._cache, stream), stream)
@@ -244,6 +246,7 @@ class HierarchyProjector(nn.Module):
                 nv.ptr(m_out), nv.ptr(lv_out), stream)
 
     def forward(self, x):
+        nv.forbid_autograd("HierarchyProjector.forward", (x,), (self,))
         x = _check_input(x)
         stream = nv.stream_of(x)
         n = x.shape[0]
@@ -300,11 +303,13 @@ class StyleGAN3Compressor(nn.Module):
         return means if deterministic else w_plus
 
     def compress(self, x, quantization_bits=8, deterministic=True):
-        if deterministic:
-            _, w_plus, _ = self.encoder(x)
-        else:
-            w_plus, _, _ = self.encoder(x)
-        return quantize_uniform(w_plus, quantization_bits)
+        # an inference API whose output is rounded (zero gradient in the reference too): run without a graph
+        with torch.no_grad():
+            if deterministic:
+                _, w_plus, _ = self.encoder(x)
+            else:
+                w_plus, _, _ = self.encoder(x)
+            return quantize_uniform(w_plus, quantization_bits)
 
     def decompress(self, w_plus, noise_mode="const"):
         return self.generator.synthesis(w_plus, noise_mode=noise_mode)

@@ -124,6 +124,32 @@ def codebook_lookup(codes, n_embeddings=256):
     return codebook(n_embeddings)[codes.reshape(-1)].reshape(codes.shape)
 
 
+def gumbel_noise(seed, m, k=256):
+    """The noise ``F.gumbel_softmax`` draws inside ``GumbelSoftmaxDiscretization.forward``
+    (``gumbel_softmax_compression.py:103-108``) right after ``torch.manual_seed(seed)``: the forward
+    consumes no CPU RNG before it; the draw is ``-empty_like(logits).exponential_().log()`` on [m, k]."""
+    g = torch.Generator().manual_seed(seed)
+    return -torch.empty(m, k).exponential_(generator=g).log()
+
+
+def gumbel_forward(z, noise, tau, hard, n_embeddings=256):
+    """``GumbelSoftmaxDiscretization.forward`` (``gumbel_softmax_compression.py:73-129``) with the Gumbel
+    noise given: distances (``:97``), ``F.gumbel_softmax`` (``:103-108``, torch's own op order: (logits +
+    g) / tau, softmax, straight-through one-hot at the argmax when hard), disc = soft @ codebook
+    (``:112``), argmin indices (``:118``), perplexity of soft.mean(0) (``:126-127``)."""
+    cb = codebook(n_embeddings)
+    d = torch.abs(z.reshape(-1, 1).float() - cb.reshape(1, -1))
+    logits = -d
+    y = ((logits + noise) / tau).softmax(1)
+    if hard:
+        y = torch.zeros_like(logits).scatter_(1, y.max(1, keepdim=True)[1], 1.0) - y + y
+    disc = torch.matmul(y, cb.reshape(-1, 1)).reshape(z.shape)
+    idx = torch.argmin(d, dim=1)
+    avg = y.mean(0)
+    perplexity = torch.exp(-torch.sum(avg * torch.log(avg + 1e-10)))
+    return disc, perplexity, idx
+
+
 def perplexity_from_hist(hist):
     """Perplexity of hard one-hot assignments: p = hist / total; exp(-sum p log(p + 1e-10))
     (``gumbel_softmax_compression.py:126-127`` evaluated on the hard one-hot)."""

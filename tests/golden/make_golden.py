@@ -169,14 +169,64 @@ def gen_containers(ref_full, ref_gumbel, enc_small):
     print("containers", stats, gstats)
 
 
-def main():
+GUMBEL_CASES = [  # (learnable_temp, temperature, hard, torch seed of the forward)
+    (True, 1.0, False, 101),
+    (True, 0.7, True, 102),
+    (False, 0.7, False, 103),
+    (False, 2.5, True, 104),
+]
+
+
+def gumbel_noise(seed, m, k):
+    """The Gumbel noise F.gumbel_softmax draws inside GumbelSoftmaxDiscretization.forward
+    (gumbel_softmax_compression.py:103-108) when the forward runs right after torch.manual_seed(seed):
+    the forward consumes no other CPU RNG before it, and gumbel_softmax draws
+    -empty_like(logits).exponential_().log() on the [m, k] logits."""
+    torch.manual_seed(seed)
+    return -torch.empty(m, k).exponential_().log()
+
+
+def gen_gumbel(ref_gumbel):
+    """Reference GumbelSoftmaxDiscretization.forward (soft / hard, learnable / fixed temperature, tau != 1):
+    z, the outputs (disc, perplexity, indices), and the seed + sha256 of the noise it drew (the test
+    regenerates the noise from the seed and checks the hash, so the fixture stays small)."""
+    g = torch.Generator().manual_seed(4321)
+    z = (torch.rand(1, 8, 32, generator=g) * 2.4 - 1.2).float()
+    m, k = z.numel(), 256
+    out = {"z": z.numpy()}
+    for ci, (learn, tau, hard, seed) in enumerate(GUMBEL_CASES):
+        disc_mod = ref_gumbel.GumbelSoftmaxDiscretization(32, k, temperature=tau, learnable_temp=learn).eval()
+        torch.manual_seed(seed)
+        with quiet(), torch.no_grad():
+            disc, perp, idx = disc_mod(z, hard=hard)
+        noise = gumbel_noise(seed, m, k)
+        # the replay reproduces the reference's output exactly (same op order as F.gumbel_softmax)
+        logits = -torch.abs(z.reshape(-1, 1) - disc_mod.codebook.reshape(1, -1))
+        y = ((logits + noise) / disc_mod.temperature).softmax(1)
+        if hard:
+            y = torch.zeros_like(logits).scatter_(1, y.max(1, keepdim=True)[1], 1.0) - y + y
+        assert torch.equal(torch.matmul(y, disc_mod.codebook.reshape(-1, 1)).reshape(z.shape), disc), ci
+        out[f"c{ci}_disc"] = disc.numpy()
+        out[f"c{ci}_perplexity"] = perp.numpy()
+        out[f"c{ci}_idx"] = idx.numpy().astype(np.int64)
+        out[f"c{ci}_noise_sha256"] = np.frombuffer(hashlib.sha256(noise.numpy().tobytes()).digest(), np.uint8)
+        out[f"c{ci}_meta"] = np.array([float(learn), tau, float(hard), float(seed)], np.float64)
+    np.savez_compressed(os.path.join(OUT, "gumbel_forward.npz"), **out)
+    print("gumbel_forward.npz", len(GUMBEL_CASES), "cases")
+
+
+def main(only=None):
     ref_full, ref_gumbel = import_reference()
+    if only == "gumbel":
+        gen_gumbel(ref_gumbel)
+        return
     gen_quantizers(ref_full, ref_gumbel)
     enc_small = gen_encoder_small(ref_full)
     gen_containers(ref_full, ref_gumbel, enc_small)
     gen_encoder_full(ref_full)
+    gen_gumbel(ref_gumbel)
 
 
 if __name__ == "__main__":
     with tempfile.TemporaryDirectory():
-        main()
+        main(sys.argv[1] if len(sys.argv) > 1 else None)

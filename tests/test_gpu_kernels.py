@@ -19,6 +19,13 @@ from oracle import sg3
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _inference():
+    """Inference tests: the HIP forwards refuse to run with grad required (nv.forbid_autograd)."""
+    with torch.no_grad():
+        yield
+
+
 def _maxdiff(a, b):
     return (a.detach().float().cpu() - b.detach().float().cpu()).abs().max().item()
 
@@ -60,19 +67,11 @@ def test_codebook_lookup_and_oob(cuda):
     codes[0, 0, 0] = 300
     _, flag = gsc.codebook_lookup(codes.to(cuda), cb)
     assert flag.item() == 1
-
-
-def _gumbel_oracle(z, noise, tau, hard):
-    cb = oe.codebook()
-    logits = -torch.abs(z.reshape(-1, 1) - cb.reshape(1, -1))
-    y = (logits + noise) / tau
-    soft = y.softmax(1)
-    if hard:
-        index = soft.max(1, keepdim=True)[1]
-        ret = torch.zeros_like(logits).scatter_(1, index, 1.0) - soft + soft
-    else:
-        ret = soft
-    return ret @ cb, ret.mean(0), torch.argmin(torch.abs(z.reshape(-1, 1) - cb.reshape(1, -1)), 1)
+    with pytest.raises(IndexError):
+        gsc.check_codes(flag, 256)
+    codes[0, 0, 0] = -1
+    _, flag = gsc.codebook_lookup(codes.to(cuda), cb)
+    assert flag.item() == 1
 
 
 @pytest.mark.parametrize("hard", [False, True])
@@ -82,11 +81,31 @@ def test_gumbel_softmax_with_given_noise(cuda, hard):
     noise = -torch.empty(z.numel(), 256).exponential_(generator=g).log()
     disc_mod = ic2.GumbelSoftmaxDiscretization(64, 256, temperature=0.7).to(cuda)
     disc, perp, idx = disc_mod(z.to(cuda), hard=hard, gumbel_noise=noise.to(cuda))
-    rdisc, ravg, ridx = _gumbel_oracle(z, noise, 0.7, hard)
+    rdisc, rperp, ridx = oe.gumbel_forward(z, noise, torch.exp(torch.ones(1) * np.log(0.7)), hard)
     assert torch.equal(idx.cpu(), ridx)
-    assert _maxdiff(disc.reshape(-1), rdisc.reshape(-1)) < 1e-5
-    rperp = torch.exp(-torch.sum(ravg * torch.log(ravg + 1e-10)))
+    assert _maxdiff(disc, rdisc) < 1e-5
     assert abs(perp.item() - rperp.item()) < 1e-3 * rperp.item()
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_gumbel_forward_matches_reference_golden(cuda, golden_dir, case):
+    """The fused Gumbel kernel fed the noise the REFERENCE drew (replayed from its seed; the hash pins the
+    replay) against the reference's own outputs (tests/golden/gumbel_forward.npz, made by make_golden.py
+    from gumbel_softmax_compression.py:73-129): soft / hard, learnable / fixed temperature, tau != 1."""
+    import hashlib
+    d = np.load(os.path.join(golden_dir, "gumbel_forward.npz"))
+    learn, tau, hard, seed = d[f"c{case}_meta"]
+    z = torch.from_numpy(d["z"])
+    noise = oe.gumbel_noise(int(seed), z.numel())
+    assert hashlib.sha256(noise.numpy().tobytes()).digest() == d[f"c{case}_noise_sha256"].tobytes()
+    mod = ic2.GumbelSoftmaxDiscretization(z.shape[-1], 256, temperature=float(tau), learnable_temp=bool(learn))
+    mod = mod.to(cuda).eval()
+    with torch.no_grad():
+        disc, perp, idx = mod(z.to(cuda), hard=bool(hard), gumbel_noise=noise.to(cuda))
+    assert torch.equal(idx.cpu(), torch.from_numpy(d[f"c{case}_idx"]))
+    assert _maxdiff(disc, torch.from_numpy(d[f"c{case}_disc"])) < 2e-6
+    rp = float(d[f"c{case}_perplexity"])
+    assert abs(perp.item() - rp) < 1e-4 * rp
 
 
 def test_gumbel_softmax_generated_noise_statistics(cuda):
@@ -241,8 +260,8 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad):
     _conv_case(cin, cout, size, pad)
 
 
-@pytest.mark.parametrize("cin_p,n,size", [(32, 2, 67), (64, 1, 40), (128, 3, 33)])
-def test_torgb_1x1_nchw(cuda, cin_p, n, size):
+@pytest.mark.parametrize("cin_p,n,size,pad", [(32, 2, 67, 0), (64, 1, 40, 0), (128, 3, 33, 0), (64, 2, 21, 1)])
+def test_torgb_1x1_nchw(cuda, cin_p, n, size, pad):
     """ToRGB (1x1 conv to 3 channels, bf16 NHWC in, NCHW f32 out with per-sample oscale, bias, clamp and
     out_mul: the SynthesisLayer L14 call) against an fp64 reference on the same bf16 operands."""
     g = torch.Generator().manual_seed(cin_p + size)
@@ -250,12 +269,14 @@ def test_torgb_1x1_nchw(cuda, cin_p, n, size):
     w = (torch.randn(32, cin_p, generator=g) / np.sqrt(cin_p)).to(torch.bfloat16)
     osc = torch.rand(n, 32, generator=g) + 0.5
     bias = torch.randn(32, generator=g)
-    y = torch.empty(n, 3, size, size, device=cuda)
+    so = size + 2 * pad  # a padded 1x1 (not the ToRGB kernel's shape) must take the implicit GEMM
+    y = torch.empty(n, 3, so, so, device=cuda)
     xd, wd, od, bd = x.to(cuda), w.to(cuda), osc.to(cuda), bias.to(cuda)
-    nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), nv.BF16, nv.F32, n, size, size, cin_p, 32, 3, 1, 1, 0, size,
-                  size, nv.ptr(od), nv.ptr(bd), nv.ACT_LRELU, 1.0, 1.0, 8.0, 0.25, nv.NCHW, nv.stream_of(xd), cuda)
+    nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), nv.BF16, nv.F32, n, size, size, cin_p, 32, 3, 1, 1, pad, so,
+                  so, nv.ptr(od), nv.ptr(bd), nv.ACT_LRELU, 1.0, 1.0, 8.0, 0.25, nv.NCHW, nv.stream_of(xd), cuda)
     torch.cuda.synchronize()
-    acc = torch.einsum("nhwc,oc->nohw", x.double(), w.double()[:3])
+    xp = torch.nn.functional.pad(x.double(), (0, 0, pad, pad, pad, pad))
+    acc = torch.einsum("nhwc,oc->nohw", xp, w.double()[:3])
     r = (acc * osc.double()[:, :3, None, None] + bias.double()[None, :3, None, None]).clamp(-8, 8) * 0.25
     assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item())
 

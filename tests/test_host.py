@@ -47,8 +47,33 @@ def test_product_path_refuses_cpu_tensors():
     with pytest.raises(RuntimeError, match="ROCm"):
         ic2.quantize_uniform(torch.zeros(4, 16, 512))
     enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32, w_dim=32)
-    with pytest.raises(RuntimeError, match="ROCm"):
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm"):
         enc(torch.zeros(1, 3, 32, 32))
+
+
+def test_forwards_refuse_autograd():
+    """No silent loss of autograd (reference training loop stylegan3_hvae_full.py:669-696): with grad mode on
+    and a parameter or input requiring grad, every HIP forward raises before touching the device."""
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32, w_dim=32)
+    x = torch.zeros(1, 3, 32, 32)
+    with pytest.raises(nv.AutogradUnsupported):
+        enc(x)
+    with pytest.raises(nv.AutogradUnsupported):
+        enc.blocks[0](torch.zeros(1, 32, 8, 8))
+    G = ic2.Generator(img_resolution=256)
+    ws = torch.zeros(1, 16, 512)
+    with pytest.raises(nv.AutogradUnsupported):
+        G.synthesis(ws)                          # parameters require grad
+    G.requires_grad_(False)
+    with pytest.raises(nv.AutogradUnsupported):
+        G.synthesis(ws.requires_grad_(True))     # the input requires grad (grads into W+)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        G.synthesis(ws.detach())                 # frozen and no input grad: reaches the device check
+    disc = ic2.GumbelSoftmaxDiscretization(32, 256)   # learnable temperature
+    with pytest.raises(nv.AutogradUnsupported):
+        disc(torch.zeros(1, 16, 32))
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm"):
+        disc(torch.zeros(1, 16, 32))
 
 
 # ------------------------------------------------------------------ seeded construction = reference

@@ -41,6 +41,24 @@ def test_closed_form_is_not_the_reference(golden_dir):
     assert (closed != d["codebook_idx"]).sum() > 0
 
 
+@pytest.mark.parametrize("case", range(4))
+def test_gumbel_forward_matches_reference(golden_dir, case):
+    """GumbelSoftmaxDiscretization.forward (gumbel_softmax_compression.py:73-129) captured from the reference
+    (soft / hard, learnable / fixed temperature, tau != 1): the replayed noise hashes to what the reference
+    drew, and the restatement reproduces disc, perplexity and indices bit for bit."""
+    import hashlib
+    d = _load(golden_dir, "gumbel_forward.npz")
+    learn, tau, hard, seed = d[f"c{case}_meta"]
+    z = torch.from_numpy(d["z"])
+    noise = oe.gumbel_noise(int(seed), z.numel())
+    assert hashlib.sha256(noise.numpy().tobytes()).digest() == d[f"c{case}_noise_sha256"].tobytes()
+    tau_t = torch.exp(torch.ones(1) * np.log(tau))  # the module's temperature = exp(log(tau)) (:63-65)
+    disc, perp, idx = oe.gumbel_forward(z, noise, tau_t, bool(hard))
+    assert torch.equal(disc, torch.from_numpy(d[f"c{case}_disc"]))
+    assert torch.equal(perp, torch.from_numpy(d[f"c{case}_perplexity"]))
+    assert torch.equal(idx, torch.from_numpy(d[f"c{case}_idx"]))
+
+
 # ------------------------------------------------------------------ encoder vs reference goldens
 def test_encoder_small_matches_reference(golden_dir):
     d = _load(golden_dir, "encoder_small.npz")
