@@ -171,9 +171,9 @@ def gen_containers(ref_full, ref_gumbel, enc_small):
 
 GUMBEL_CASES = [  # (learnable_temp, temperature, hard, torch seed of the forward)
     (True, 1.0, False, 101),
-    (True, 0.7, True, 102),
-    (False, 0.7, False, 103),
-    (False, 2.5, True, 104),
+    (True, 0.7, True, 101),
+    (False, 0.7, False, 101),
+    (False, 2.5, True, 101),
 ]
 
 
@@ -188,8 +188,10 @@ def gumbel_noise(seed, m, k):
 
 def gen_gumbel(ref_gumbel):
     """Reference GumbelSoftmaxDiscretization.forward (soft / hard, learnable / fixed temperature, tau != 1):
-    z, the outputs (disc, perplexity, indices), and the seed + sha256 of the noise it drew (the test
-    regenerates the noise from the seed and checks the hash, so the fixture stays small)."""
+    z, the outputs (disc, perplexity, indices), and the noise it drew.  Every case runs after the same seed,
+    so one stored noise array serves all four (the CPU exponential_ stream is not bit-identical across
+    host CPUs -- AVX2 vs AVX-512 -- so the GPU box cannot regenerate it; the sha256 lets a host check its
+    own replay)."""
     g = torch.Generator().manual_seed(4321)
     z = (torch.rand(1, 8, 32, generator=g) * 2.4 - 1.2).float()
     m, k = z.numel(), 256
@@ -209,6 +211,7 @@ def gen_gumbel(ref_gumbel):
         out[f"c{ci}_disc"] = disc.numpy()
         out[f"c{ci}_perplexity"] = perp.numpy()
         out[f"c{ci}_idx"] = idx.numpy().astype(np.int64)
+        out["noise"] = noise.numpy()
         out[f"c{ci}_noise_sha256"] = np.frombuffer(hashlib.sha256(noise.numpy().tobytes()).digest(), np.uint8)
         out[f"c{ci}_meta"] = np.array([float(learn), tau, float(hard), float(seed)], np.float64)
     np.savez_compressed(os.path.join(OUT, "gumbel_forward.npz"), **out)

