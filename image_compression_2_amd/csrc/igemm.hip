@@ -604,6 +604,250 @@ static void launch_g8(IgemmArgs a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Halo implicit GEMM for the wide 3x3 layers (bf16, cin_p % 64 == 0): the modulated convs of SG3 synthesis
+// and the encoder's wide blocks.  The implicit GEMM above stages a shifted 256-pixel panel per tap, so every
+// input pixel crosses L2 -> LDS nine times per 64-channel block; here the output tile is a 2-D block of
+// TH x TW = 256 pixels of one sample, and its (TH+2) x (TW+2) input halo is staged ONCE per 64-channel block
+// (1.27-1.33x the pixels instead of 9x) and read at nine shifted offsets from LDS.  Only the weight slab
+// (BO output channels x one tap x 64 channels) is streamed per K-step.
+//   bytes per 64-channel block per tile: 9 x BO x 128 B (weights) + halo  -> 229 FLOP/B at BO 256 vs 128
+// 8 waves, each owning 128 output channels x (256 OG / 8) pixels: OG = 2: 2 o-groups x 4 p-groups (64 px);
+// OG = 1: 8 p-groups of 32 px.  LDS: 2 weight slabs (ring) + 2 halos (the next block's halo lands by LDS-DMA
+// behind the current block's 9 taps), rows of 128 B with the 16-B chunk XOR swizzle of the 8-phase kernels.
+// K-step t = (block cb = t / 9, tap = t % 9): barrier; fragment reads; DMA of step t+1's weight slab (and at
+// tap 0 of the next block's halo); 64 (OG 2) / 32 (OG 1) MFMAs per wave; vmcnt(0).
+// Output channel rows wholly in the padding (cout_p 192 / 384 tails) skip their MFMAs.
+static bool ig_env_off(const char* name);
+
+template <int OG, int TW>
+struct HG {
+  static constexpr int BO = 128 * OG, TH = 256 / TW;
+  static constexpr int HW = TW + 2, HH = TH + 2, NH = HH * HW;  // halo pixels
+  static constexpr int NHI = (NH + 7) / 8;                      // 1-KiB DMA instructions per halo (8 px each)
+  static constexpr int HPW = (NHI + 7) / 8;                     // per wave, at most
+  static constexpr int HALO_B = NHI * 1024;
+  static constexpr int WS_B = BO * 128;                         // one weight slab: BO rows x 64 channels
+  static constexpr int NWI = BO / 64;                           // weight DMA instructions per wave
+  static constexpr int J = 2 * OG;                              // 16-pixel blocks per wave
+  static constexpr int LDS_B = 2 * WS_B + 2 * HALO_B;
+};
+
+template <int OG, int TW>
+__device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
+  using G = HG<OG, TW>;
+  constexpr int J = G::J, NWI = G::NWI, HPW = G::HPW;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
+  char* const wsl = lds;                    // 2 weight slabs
+  char* const hal = lds + 2 * G::WS_B;      // 2 halos
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int og = OG == 2 ? wid >> 2 : 0;
+  const int pg = OG == 2 ? wid & 3 : wid;
+  const int fr = lane & 15, fh = lane >> 4;
+
+  // tile: o fastest (the o-tiles of one pixel tile share its halo in L2), XCD-aware
+  const int logical = xcd_remap(blockIdx.x, a.nblocks);
+  const int o_tile = logical % a.tiles_o;
+  int pt = logical / a.tiles_o;
+  const int tx = pt % tiles_x;
+  pt /= tiles_x;
+  const int ty = pt % tiles_y;
+  const int nn = pt / tiles_y;
+  const int o0 = o_tile * G::BO;
+  const int oy0 = ty * G::TH, ox0 = tx * TW;
+
+  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
+  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  // weight DMA: instruction k of this wave fills slab rows (wid + 8k) * 8 + lrow; per-lane offset is constant
+  // across K-steps (the step's (tap, block) part is the descriptor base)
+  uint32_t w_off[NWI];
+#pragma unroll
+  for (int k = 0; k < NWI; ++k) {
+    const int row = (wid + 8 * k) * 8 + lrow;
+    const int o = o0 + row;
+    w_off[k] = o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((row >> 1) & 7)) << 4)) : kOob;
+  }
+  // halo DMA: instruction g = wid + 8k moves halo pixels g*8 .. g*8+7; offset of the pixel's 64-channel
+  // block 0 (the block index is in the descriptor base); outside the image / past the halo -> kOob (zeros)
+  uint32_t h_off[HPW];
+#pragma unroll
+  for (int k = 0; k < HPW; ++k) {
+    const int g = wid + 8 * k;
+    const int hp = g * 8 + lrow;
+    const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
+    const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
+    const bool ok = g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
+    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ ((hp >> 1) & 7)) << 3)) * 2) : kOob;
+  }
+  // B fragment rows: pixel block pb = pg * J + j -> tile pixel (py, px0 + fr); halo row at tap (0, 0)
+  int brow[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pb = pg * J + j;
+    const int py = pb * 16 / TW, px = (pb * 16) % TW + fr;
+    brow[j] = py * G::HW + px;
+  }
+  const int obase = og * 128;
+  const bool live0 = o0 + obase < a.cout_p, live1 = o0 + obase + 64 < a.cout_p;
+  const int CB = a.cin_p >> 6;
+  const int nq = CB * 9;
+
+  auto issue_w = [&](int t) {  // weight slab of K-step t -> slab t & 1
+    const int cb = t / 9, tap = t - (t / 9) * 9;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(wg + ((int64_t)tap * a.cin_p + cb * 64) * 2), 0, t < nq ? kOob : 0, kRsrcWord3);
+    char* dst = wsl + (t & 1) * G::WS_B;
+#pragma unroll
+    for (int k = 0; k < NWI; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
+                                               16, w_off[k], 0, 0, 0);
+  };
+  auto issue_h = [&](int cb) {  // halo of block cb -> halo cb & 1
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 128), 0, kOob, kRsrcWord3);
+    char* dst = hal + (cb & 1) * G::HALO_B;
+#pragma unroll
+    for (int k = 0; k < HPW; ++k)
+      if (wid + 8 * k < G::NHI)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
+                                                 16, h_off[k], 0, 0, 0);
+  };
+
+  f32x4 acc[8][J];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_h(0);
+  issue_w(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int t = 0; t < nq; ++t) {
+    __builtin_amdgcn_s_barrier();  // step t's slab and block t/9's halo landed for every wave; step t-1 read
+    __builtin_amdgcn_sched_barrier(0);
+    const int cb = t / 9, tap = t - (t / 9) * 9;
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    const char* wl = wsl + (t & 1) * G::WS_B;
+    const char* hl = hal + (cb & 1) * G::HALO_B;
+    bf16x8 af[8][2], bfr[J][2];
+    if (live0) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int row = brow[j] + ky * G::HW + kx;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) bfr[j][s] = *reinterpret_cast<const bf16x8*>(hl + g8_off(row, 4 * s + fh));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = *reinterpret_cast<const bf16x8*>(wl + g8_off(obase + i * 16 + fr, 4 * s + fh));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nq) issue_w(t + 1);               // slab (t+1) & 1 was read by step t-1 (before the barrier)
+    if (tap == 0 && cb + 1 < CB) issue_h(cb + 1);  // halo (cb+1) & 1 was read by block cb-1
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if (live0) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (live1) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 4; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for step t+1 landed
+  }
+
+  // epilogue: lane holds C[o = o0 + obase + 16 i + 4 fh + r][tile pixel (pb, fr)]
+  const int hw = a.ho * a.wo;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pb = pg * J + j;
+    const int oy = oy0 + pb * 16 / TW, ox = ox0 + (pb * 16) % TW + fr;
+    if (oy >= a.ho || ox >= a.wo) continue;
+    const int pix = oy * a.wo + ox;
+    const int p = nn * hw + pix;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ob = o0 + obase + i * 16 + 4 * fh;
+      if (ob >= a.cout_p) continue;
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      ig_store4(a, p, nn, pix, ob, v);
+    }
+  }
+}
+
+// one non-template kernel per instance (a __global__ template's host stub is not emitted here)
+__global__ void __launch_bounds__(512, 1) hgemm_o2_w32_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<2, 32>(a, tx, ty); }
+__global__ void __launch_bounds__(512, 1) hgemm_o2_w16_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<2, 16>(a, tx, ty); }
+__global__ void __launch_bounds__(512, 1) hgemm_o1_w32_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<1, 32>(a, tx, ty); }
+__global__ void __launch_bounds__(512, 1) hgemm_o1_w16_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<1, 16>(a, tx, ty); }
+
+template <int OG, int TW>
+static void launch_hgemm(IgemmArgs a, hipStream_t s) {
+  using G = HG<OG, TW>;
+  const int tiles_x = (int)ceil_div(a.wo, TW), tiles_y = (int)ceil_div(a.ho, G::TH);
+  a.tiles_o = (a.cout_p + G::BO - 1) / G::BO;
+  a.nblocks = a.n * tiles_x * tiles_y * a.tiles_o;
+  const dim3 grid(a.nblocks), block(512);
+  if (OG == 2 && TW == 32) hipLaunchKernelGGL(hgemm_o2_w32_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
+  else if (OG == 2) hipLaunchKernelGGL(hgemm_o2_w16_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
+  else if (TW == 32) hipLaunchKernelGGL(hgemm_o1_w32_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
+  else hipLaunchKernelGGL(hgemm_o1_w16_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
+}
+
+// instance choice: pixel tile 16 x 16 or 8 x 32, whichever pads the output less; 256 output channels per
+// workgroup when cout_p is a multiple of 256 (or 192: one o-tile, its last 64 rows skipped), else 128
+struct HgPlan {
+  bool tw32, og2;
+  int64_t blocks;
+};
+static HgPlan hg_plan(int n, int ho, int wo, int cout_p) {
+  const int64_t a16 = ceil_div(ho, 16) * 16 * ceil_div(wo, 16) * 16;
+  const int64_t a32 = ceil_div(ho, 8) * 8 * ceil_div(wo, 32) * 32;
+  HgPlan p;
+  p.tw32 = a32 <= a16;
+  p.og2 = cout_p % 256 == 0 || cout_p == 192;
+  const int64_t tiles = p.tw32 ? ceil_div(ho, 8) * ceil_div(wo, 32) : ceil_div(ho, 16) * ceil_div(wo, 16);
+  p.blocks = n * tiles * ceil_div(cout_p, p.og2 ? 256 : 128);
+  return p;
+}
+
+// bf16 3x3 with 64-deep channel blocks whose buffer offsets fit 31 bits, on a grid of >= ~1 workgroup per CU
+// (smaller launches keep the split-K implicit GEMM); IC2_HGEMM=0 keeps them all on the implicit GEMM
+static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
+  static const bool on = !ig_env_off("IC2_HGEMM");
+  if (!(on && dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 64 == 0 && cout_p % 64 == 0 &&
+        x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))
+    return false;
+  return hg_plan(n, ho, wo, cout_p).blocks >= 240;
+}
+
+static void hgemm_dispatch(const IgemmArgs& a, hipStream_t s) {
+  const HgPlan p = hg_plan(a.n, a.ho, a.wo, a.cout_p);
+  if (p.og2) {
+    if (p.tw32) launch_hgemm<2, 32>(a, s);
+    else launch_hgemm<2, 16>(a, s);
+  } else {
+    if (p.tw32) launch_hgemm<1, 32>(a, s);
+    else launch_hgemm<1, 16>(a, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launch plan: tile instance and K split.  Tile ids: 0 = f32 128x128 (2-stage); bf16: 1 = 256x256,
 // 2 = 32x256, 3 = 128x256, 4 = 128x128, 5 = 64x256 (4-stage ring), 6 = 8-phase 256x256, 7 = 8-phase 128x512.
 // IC2_IGEMM_TILE=1..7 forces a bf16 tile (tests exercise every instance on small problems),
@@ -896,6 +1140,9 @@ extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int 
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
   const int64_t M = (int64_t)n * ho * wo;
+  if (hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo) &&
+      !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw))
+    return 0;
   const IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   return pl.splits > 1 ? (int64_t)pl.splits * M * cout_p * 4 : 0;
 }
@@ -938,9 +1185,14 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype);
+  const bool hconv = !torgb && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
+  const bool hgemm = !torgb && !hconv && hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
+  if (hgemm) pl.splits = 1;
   if (torgb) {
     launch_torgb(a, s);
-  } else if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
+  } else if (hgemm) {
+    hgemm_dispatch(a, s);
+  } else if (hconv) {
     if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
     else if (cin_p == 32) launch_hconv<32, 64>(a, s);
     else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
@@ -960,7 +1212,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   } else {
     launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
   }
-  if (pl.splits > 1 && !torgb && !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) {
+  if (pl.splits > 1 && !torgb && !hconv && !hgemm) {
     const int64_t total = M * (cout_p / 4);
     const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
     hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);

@@ -260,6 +260,16 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad):
     _conv_case(cin, cout, size, pad)
 
 
+@pytest.mark.parametrize("cin,cout,size,pad", [(64, 256, 62, 1), (128, 512, 45, 2), (192, 192, 45, 1), (64, 128, 62, 2),
+                                              (256, 384, 40, 1), (128, 181, 40, 2), (384, 256, 40, 2)])
+def test_conv_halo_gemm(cuda, cin, cout, size, pad):
+    """The halo implicit GEMM (bf16 3x3, cin_p % 64 == 0: 2-D pixel tiles whose input halo is staged once
+    per 64-channel block) on every instance -- 256 / 128 output channels per workgroup, 16 x 16 / 8 x 32 pixel
+    tiles, padded output-channel tails (181 -> 192, 384), ragged tile edges, pad 1 and 2 -- against
+    F.conv2d in fp64."""
+    _conv_case(cin, cout, size, pad, n=8)
+
+
 @pytest.mark.parametrize("cin_p,n,size,pad", [(32, 2, 67, 0), (64, 1, 40, 0), (128, 3, 33, 0), (64, 2, 21, 1)])
 def test_torgb_1x1_nchw(cuda, cin_p, n, size, pad):
     """ToRGB (1x1 conv to 3 channels, bf16 NHWC in, NCHW f32 out with per-sample oscale, bias, clamp and
@@ -281,13 +291,13 @@ def test_torgb_1x1_nchw(cuda, cin_p, n, size, pad):
     assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item())
 
 
-def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16):
+def _conv_case(cin, cout, size, pad, dtype=torch.bfloat16, n=3):
     cuda = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(cin + cout)
     conv = torch.nn.Conv2d(cin, cout, 3, padding=pad)
     with torch.no_grad():
         conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
-    x = torch.randn(3, cin, size, size, generator=g)
+    x = torch.randn(n, cin, size, size, generator=g)
     convg = conv.to(cuda)
     stream = nv.stream_of(x.to(cuda))
     y = _to_nchw(_conv(convg, _to_nhwc(x.to(cuda), dtype, stream), dtype, {}, stream), stream)
