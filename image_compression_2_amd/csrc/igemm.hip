@@ -635,20 +635,15 @@ struct HG {
 template <int OG, int TW>
 __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = HG<OG, TW>;
-  constexpr int J = G::J;
-  constexpr int NWF = G::BO / 32;              // weight DMA instructions per front wave (4 waves move BO rows)
-  constexpr int NHB = (G::NHI + 3) / 4;        // halo DMA instructions per back wave
-  constexpr int ND = NWF > NHB ? NWF : NHB;    // per-lane DMA offsets (role-dependent meaning)
+  constexpr int J = G::J, NWI = G::NWI, HPW = G::HPW;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
   char* const wsl = lds;                    // 2 weight slabs
   char* const hal = lds + 2 * G::WS_B;      // 2 halos
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int half = wid >> 2;                // 0: front waves (weight DMA), 1: back waves (halo DMA, one barrier behind)
-  const int w4 = wid & 3;
-  const int og = OG == 2 ? half : 0;
-  const int pg = OG == 2 ? w4 : wid;
+  const int og = OG == 2 ? wid >> 2 : 0;
+  const int pg = OG == 2 ? wid & 3 : wid;
   const int fr = lane & 15, fh = lane >> 4;
 
   // tile: o fastest (the o-tiles of one pixel tile share its halo in L2), XCD-aware
@@ -666,24 +661,26 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
   const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
   const int lrow = lane >> 3, pch = lane & 7;
 
-  // per-lane DMA offsets, constant across K-steps (the step's (tap, block) part is the descriptor base):
-  //  front wave w4, instruction k: weight slab rows (w4 + 4k) * 8 + lrow;
-  //  back wave w4, instruction k:  halo pixels g * 8 + lrow, g = w4 + 4k (kOob outside the image / halo)
-  uint32_t doff[ND];
+  // weight DMA: instruction k of this wave fills slab rows (wid + 8k) * 8 + lrow; per-lane offset is constant
+  // across K-steps (the step's (tap, block) part is the descriptor base)
+  uint32_t w_off[NWI];
 #pragma unroll
-  for (int k = 0; k < ND; ++k) {
-    if (half == 0) {
-      const int row = (w4 + 4 * k) * 8 + lrow;
-      const int o = o0 + row;
-      doff[k] = k < NWF && o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((row >> 1) & 7)) << 4)) : kOob;
-    } else {
-      const int g = w4 + 4 * k;
-      const int hp = g * 8 + lrow;
-      const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
-      const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
-      const bool ok = k < NHB && g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
-      doff[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ ((hp >> 1) & 7)) << 3)) * 2) : kOob;
-    }
+  for (int k = 0; k < NWI; ++k) {
+    const int row = (wid + 8 * k) * 8 + lrow;
+    const int o = o0 + row;
+    w_off[k] = o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((row >> 1) & 7)) << 4)) : kOob;
+  }
+  // halo DMA: instruction g = wid + 8k moves halo pixels g*8 .. g*8+7; offset of the pixel's 64-channel
+  // block 0 (the block index is in the descriptor base); outside the image / past the halo -> kOob (zeros)
+  uint32_t h_off[HPW];
+#pragma unroll
+  for (int k = 0; k < HPW; ++k) {
+    const int g = wid + 8 * k;
+    const int hp = g * 8 + lrow;
+    const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
+    const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
+    const bool ok = g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
+    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ ((hp >> 1) & 7)) << 3)) * 2) : kOob;
   }
   // B fragment rows: pixel block pb = pg * J + j -> tile pixel (py, px0 + fr); halo row at tap (0, 0)
   int brow[J];
@@ -698,25 +695,25 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
   const int CB = a.cin_p >> 6;
   const int nq = CB * 9;
 
-  auto issue_w = [&](int t) {  // front waves: weight slab of K-step t -> slab t & 1
+  auto issue_w = [&](int t) {  // weight slab of K-step t -> slab t & 1
     const int cb = t / 9, tap = t - (t / 9) * 9;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(wg + ((int64_t)tap * a.cin_p + cb * 64) * 2), 0, kOob, kRsrcWord3);
+        (void*)(wg + ((int64_t)tap * a.cin_p + cb * 64) * 2), 0, t < nq ? kOob : 0, kRsrcWord3);
     char* dst = wsl + (t & 1) * G::WS_B;
 #pragma unroll
-    for (int k = 0; k < NWF; ++k)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (w4 + 4 * k) * 1024),
-                                               16, doff[k], 0, 0, 0);
+    for (int k = 0; k < NWI; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
+                                               16, w_off[k], 0, 0, 0);
   };
-  auto issue_h = [&](int cb) {  // back waves: halo of block cb -> halo cb & 1
+  auto issue_h = [&](int cb) {  // halo of block cb -> halo cb & 1
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 128), 0, kOob, kRsrcWord3);
     char* dst = hal + (cb & 1) * G::HALO_B;
 #pragma unroll
-    for (int k = 0; k < NHB; ++k)
-      if (w4 + 4 * k < G::NHI)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (w4 + 4 * k) * 1024),
-                                                 16, doff[k], 0, 0, 0);
+    for (int k = 0; k < HPW; ++k)
+      if (wid + 8 * k < G::NHI)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
+                                                 16, h_off[k], 0, 0, 0);
   };
 
   f32x4 acc[8][J];
@@ -725,22 +722,11 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Two barriers per K-step (B1: step t's data landed and slot (t+1) & 1 is free; B2: mid-step); the back
-  // waves run one barrier behind, so on every SIMD one wave's fragment reads overlap its partner's MFMAs.
-  //   front: B1(t) | reads(t), weight DMA(t+1), MFMA k 0-31 | B2(t) | MFMA k 32-63, vmcnt(0) |
-  //   back : B2(t-1) ...                                    | B1(t) | reads(t), halo DMA (tap 0), MFMA k 0-31 | ...
-  // WAR: slot (t+1) & 1 / halo (cb+1) & 1 were last read at step t-1 / block cb-1, whose reads every wave
-  // finished (lgkmcnt) before its next barrier.  RAW: a wave's DMA lands (vmcnt(0)) before the barrier after
-  // which any wave reads it.
-  if (half == 0) {
-    issue_w(0);
-  } else {
-    issue_h(0);
-  }
+  issue_h(0);
+  issue_w(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (half == 1) __builtin_amdgcn_s_barrier();  // back waves start one barrier behind
   for (int t = 0; t < nq; ++t) {
-    __builtin_amdgcn_s_barrier();  // B1(t)
+    __builtin_amdgcn_s_barrier();  // step t's slab and block t/9's halo landed for every wave; step t-1 read
     __builtin_amdgcn_sched_barrier(0);
     const int cb = t / 9, tap = t - (t / 9) * 9;
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
@@ -749,60 +735,41 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
     bf16x8 af[8][2], bfr[J][2];
     if (live0) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int j = 0; j < J; ++j) {
+        const int row = brow[j] + ky * G::HW + kx;
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-          const int row = brow[j] + ky * G::HW + kx;
-          bfr[j][s] = *reinterpret_cast<const bf16x8*>(hl + g8_off(row, 4 * s + fh));
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          af[i][s] = *reinterpret_cast<const bf16x8*>(wl + g8_off(obase + i * 16 + fr, 4 * s + fh));
+        for (int s = 0; s < 2; ++s) bfr[j][s] = *reinterpret_cast<const bf16x8*>(hl + g8_off(row, 4 * s + fh));
       }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = *reinterpret_cast<const bf16x8*>(wl + g8_off(obase + i * 16 + fr, 4 * s + fh));
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (half == 0) {
-      if (t + 1 < nq) issue_w(t + 1);
-    } else {
-      if (tap == 0 && cb + 1 < CB) issue_h(cb + 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    if (live0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
-    }
-    if (live1) {
-#pragma unroll
-      for (int i = 4; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step t are in registers
-    __builtin_amdgcn_s_barrier();  // B2(t)
+    if (t + 1 < nq) issue_w(t + 1);               // slab (t+1) & 1 was read by step t-1 (before the barrier)
+    if (tap == 0 && cb + 1 < CB) issue_h(cb + 1);  // halo (cb+1) & 1 was read by block cb-1
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
     if (live0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
     }
     if (live1) {
 #pragma unroll
-      for (int i = 4; i < 8; ++i)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
+        for (int i = 4; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for step t+1 landed
   }
-  if (half == 0) __builtin_amdgcn_s_barrier();  // balance the back waves' extra barrier
 
   // epilogue: lane holds C[o = o0 + obase + 16 i + 4 fh + r][tile pixel (pb, fr)]
   const int hw = a.ho * a.wo;
@@ -860,13 +827,24 @@ static HgPlan hg_plan(int n, int ho, int wo, int cout_p) {
 }
 
 // bf16 3x3 with 64-deep channel blocks whose buffer offsets fit 31 bits, on a grid of >= ~1 workgroup per CU
-// (smaller launches keep the split-K implicit GEMM); IC2_HGEMM=0 keeps them all on the implicit GEMM
+// (smaller launches keep the split-K implicit GEMM).  Measured against the 8-phase implicit GEMM on the bench
+// shapes (profiles/r2_hgemm_sweep.txt): faster on the encoder's 128^2 / 64^2 blocks and on SG3 L12 (192 -> 128
+// at 276^2), level on L11 / L13, slower on the 512-wide layers (there the 8-phase kernel's staggered halves
+// keep the matrix pipe busier than the halo saves) and wherever the 2-D tiles pad the image by > 5 %.
+// So: cin_p, cout_p <= 256 and >= 95 % tile utilisation.  IC2_HGEMM=0 disables it, =2 forces it wherever legal.
 static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
-  static const bool on = !ig_env_off("IC2_HGEMM");
-  if (!(on && dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 64 == 0 && cout_p % 64 == 0 &&
+  static const int mode = [] {
+    const char* e = getenv("IC2_HGEMM");
+    return e ? atoi(e) : 1;
+  }();
+  if (!(mode && dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 64 == 0 && cout_p % 64 == 0 &&
         x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))
     return false;
-  return hg_plan(n, ho, wo, cout_p).blocks >= 240;
+  const HgPlan p = hg_plan(n, ho, wo, cout_p);
+  if (p.blocks < 240) return false;
+  if (mode == 2) return true;
+  const double util = (double)ho * wo * n * ceil_div(cout_p, p.og2 ? 256 : 128) / (256.0 * p.blocks);
+  return cin_p <= 256 && cout_p <= 256 && util >= 0.95;
 }
 
 static void hgemm_dispatch(const IgemmArgs& a, hipStream_t s) {
