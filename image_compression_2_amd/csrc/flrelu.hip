@@ -347,7 +347,9 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
     return !(e && e[0] == '0');
   }();
   // f16 input (the synthesis conv epilogue's output) exists only for the MFMA formulation
-  const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) && dtype_out == IC2_BF16 && b == nullptr;
+  // (one polyphase phase for both axes: the instances take a single delta)
+  const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) && dtype_out == IC2_BF16 && b == nullptr &&
+                       dx == dy;
   if ((use_mfma || dtype_in == IC2_F16) && mfma_ok) {
     for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
     for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;

@@ -29,6 +29,7 @@ typedef float fm_f4 __attribute__((ext_vector_type(4)));
 typedef float fm_f2 __attribute__((ext_vector_type(2)));
 
 constexpr int FM_TAPS = 276;
+constexpr uint32_t FM_OOB = 0x7ffffff0u;  // buffer num_records = the zero-answer offset (per-sample image < 2 GiB)
 
 template <int U>
 struct FmGeom {
@@ -185,7 +186,23 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
     c0 = cb * 16;
   };
   // input tile -> in_img[jy][x][16 ch] (zeros outside the image).  The image is dense (pixel p at 32 B * p),
-  // i.e. lane-linear in (pixel, 16-B half): f16 input goes to LDS by LDS-DMA, asynchronously.
+  // i.e. lane-linear in (pixel, 16-B half): f16 input goes to LDS by LDS-DMA, asynchronously.  Which (row,
+  // column, half) a lane moves in its i-th DMA instruction does not depend on the tile: precomputed once
+  // (jy | x << 16, -1 past the image), so a tile's DMA costs a few 32-bit ops per instruction: a raw buffer
+  // load whose descriptor base is the tile's sample + channel block and whose per-lane offset is the pixel's,
+  // or FM_OOB (answered with zeros) outside the input image.
+  constexpr int NDMA = (NCH + 63) / 64;            // 1-KiB DMA instructions per tile
+  constexpr int NDW = (NDMA + NW - 1) / NW;        // per wave, at most
+  int dma_yx[NDW];
+#pragma unroll
+  for (int i = 0; i < NDW; ++i) {
+    const int k = wave + NW * i;
+    const int e = k * 64 + lane;
+    const int pix = e >> 1;
+    const int jy = pix / NIN, x = pix - (pix / NIN) * NIN;
+    dma_yx[i] = (k < NDMA && e < NCH) ? (jy | (x << 16)) : -1;
+  }
+  const int half8 = (lane & 1) * 8;
   auto chunk_src = [&](int e, int n, int sy0, int sx0, int c0) -> const void* {
     const int pix = e >> 1, half = e & 1;
     const int jy = pix / NIN, x = pix - jy * NIN;
@@ -199,10 +216,20 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
     tile_geom(t, n, oy0, ox0, c0);
     const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
     if constexpr (IN_F16) {
-      for (int k = wave; k * 64 < NCH; k += NW)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)chunk_src(k * 64 + lane, n, sy0,
-                                                                                                   sx0, c0),
-                                         (__attribute__((address_space(3))) void*)(in_img + k * 256), 16, 0, 0);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(xin + (int64_t)n * a.in_h * a.in_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NDW; ++i) {
+        const int k = wave + NW * i;
+        if (k < NDMA) {
+          const int yx = dma_yx[i];
+          const int iy = sy0 + (yx & 0xffff), ix = sx0 + (yx >> 16);
+          const bool ok = yx >= 0 && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
+          const uint32_t off = ok ? (uint32_t)(((iy * a.in_w + ix) * a.c_p + half8) * 2) : FM_OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(in_img + k * 256), 16,
+                                                   off, 0, 0, 0);
+        }
+      }
     } else {
       constexpr int PER = (NCH + NT - 1) / NT;
       uint4 v[PER];
@@ -406,6 +433,285 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wide-tile variant (f16 input, the synthesis path): one tile = one sample x 16 output rows x TOX (32)
+// output columns x 16 channels, NW (8) waves.  Per output it computes 48 x 80 / (16 x 32) = 7.5 lrelu-grid
+// points instead of 48 x 48 / 256 = 9 (the 12-tap down filter needs 2 * 31 + 12 = 74 grid columns for 32
+// outputs: 5 blocks of 16), amortises each phase's barrier over twice the outputs, and its 79 KB of LDS (the
+// tap table aliases the D image: it is only read before the first tile) keeps 2 workgroups = 16 waves per CU.
+// Same passes and per-pass matrices as flrelu_mfma_kernel; the horizontal down pass of output block ob reads
+// grid blocks 2 ob .. 2 ob + 2 with the block-0 matrices (the band is translation invariant).
+template <int U, int TOX>
+struct FmGeom2 {
+  static constexpr int TU = 6 * U, TD = 12;
+  static constexpr int RAY = 15 * 2 + TD, RAX = (TOX - 1) * 2 + TD;  // 42 x 74 grid rows x columns
+  static constexpr int NINY = (RAY + TU - 2) / U + 1, NINX = (RAX + TU - 2) / U + 1;  // up 2: 27 x 43
+  static constexpr int NBY = (RAY + 15) / 16, NBX = (RAX + 15) / 16;                   // 3 x 5 grid blocks
+  static constexpr int NOB = TOX / 16;                                                  // output column blocks
+  static constexpr int IN_PITCH = NINX * 8;  // [jy][x][16 ch] (dwords); NINX odd
+  static constexpr int NCH = NINY * NINX * 2;
+  static constexpr int IN_DW = (NCH + 63) / 64 * 256;
+  static constexpr int V_PITCH = NINX * 8 + 2;
+  static constexpr int V_DW = 16 * V_PITCH;
+  static constexpr int D_XP = 10;
+  static constexpr int D_PITCH = TOX * D_XP + 8;
+  static constexpr int D_DW = 16 * D_PITCH;
+  static constexpr int LDS_DW = IN_DW + V_DW + (D_DW > FM_TAPS ? D_DW : FM_TAPS);
+  static_assert(NINX % 2 == 1 && NINY % 2 == 1 && NINY >= 16, "input image sides must be odd and cover a window");
+  static_assert(NBX == 2 * NOB + 1, "horizontal down: output block ob reads grid blocks 2ob .. 2ob+2");
+};
+
+template <int U, int DELTA, int TOX, int NW>
+__global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int ntiles) {
+  constexpr int NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;  // grid rows per wave per block; output columns per wave
+  using G = FmGeom2<U, TOX>;
+  constexpr int NINY = G::NINY, NINX = G::NINX, NBX = G::NBX, NOB = G::NOB, NCH = G::NCH;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW];
+  uint32_t* const in_img = lds;
+  uint32_t* const v_img = lds + G::IN_DW;
+  uint32_t* const d_img = v_img + G::V_DW;
+  float* const taps = reinterpret_cast<float*>(d_img);  // read only before the first tile
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+
+  for (int i = tid; i < FM_TAPS; i += NT) {
+    float v = 0.f;
+    if (i >= 48 && i < 72) v = a.gu[i - 48];
+    else if (i >= 148 && i < 160) v = a.gd[i - 148];
+    else if (i >= 228 && i < 240) v = a.gdg[i - 228];
+    taps[i] = v;
+  }
+
+  const int slot = fm_xcd_remap(blockIdx.x, gridDim.x);
+  const uint16_t* xin = reinterpret_cast<const uint16_t*>(a.x);
+  auto tile_geom = [&](int t, int& n, int& oy0, int& ox0, int& c0) {
+    const int cb = t % a.cblocks;
+    t /= a.cblocks;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    n = t / a.tiles_y;
+    oy0 = ty * 16;
+    ox0 = tx * TOX;
+    c0 = cb * 16;
+  };
+  // per-lane DMA pattern (tile independent): jy | x << 16, -1 past the image
+  constexpr int NDMA = (NCH + 63) / 64;
+  constexpr int NDW = (NDMA + NW - 1) / NW;
+  int dma_yx[NDW];
+#pragma unroll
+  for (int i = 0; i < NDW; ++i) {
+    const int k = wave + NW * i;
+    const int e = k * 64 + lane;
+    const int pix = e >> 1;
+    const int jy = pix / NINX, x = pix - (pix / NINX) * NINX;
+    dma_yx[i] = (k < NDMA && e < NCH) ? (jy | (x << 16)) : -1;
+  }
+  const int half8 = (lane & 1) * 8;
+  auto load_tile = [&](int t) {
+    int n, oy0, ox0, c0;
+    tile_geom(t, n, oy0, ox0, c0);
+    const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(xin + (int64_t)n * a.in_h * a.in_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NDW; ++i) {
+      const int k = wave + NW * i;
+      if (k < NDMA) {
+        const int yx = dma_yx[i];
+        const int iy = sy0 + (yx & 0xffff), ix = sx0 + (yx >> 16);
+        const bool ok = yx >= 0 && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
+        const uint32_t off = ok ? (uint32_t)(((iy * a.in_w + ix) * a.c_p + half8) * 2) : FM_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(in_img + k * 256), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+  };
+  if (slot < ntiles) load_tile(slot);
+  __syncthreads();  // taps
+
+  // filter matrices (f16) in registers; y and x windows differ only through NINY / NINX clipping
+  fm_h4 gmy[3], gmx[NBX];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int w0 = fm_win<U, DELTA, NINY>(16 * t);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
+    gmy[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+#pragma unroll
+  for (int t = 0; t < NBX; ++t) {
+    const int w0 = fm_win<U, DELTA, NINX>(16 * t);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
+    gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  fm_h8 gdh01, gdh2;
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kx = (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+      v[j] = taps[228 + kx - 2 * li];
+    }
+    gdh01 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[228 + 32 + 4 * g + j - 2 * li];
+    gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), make_uint2(0u, 0u));
+  }
+  fm_h4 gdv[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[148 + 16 * b + 4 * g + j - 2 * li];
+    gdv[b] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  const float slope = a.slope, lim = a.lim;
+  const uint32_t slope2 = fm_h2u(slope, slope), lim2 = fm_h2u(lim, lim), nlim2 = fm_h2u(-lim, -lim);
+  bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
+  __syncthreads();  // every wave's tap reads are done before the first D store overwrites the table
+
+  for (int t = slot; t < ntiles; t += gridDim.x) {
+    int n, oy0, ox0, c0;
+    tile_geom(t, n, oy0, ox0, c0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA (and last tile's stores)
+    __syncthreads();                                   // everyone's; and the previous tile fully consumed
+
+    fm_f4 acc[OCW];
+#pragma unroll
+    for (int i = 0; i < OCW; ++i) acc[i] = fm_f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      // ---- vertical up: V^T[c][ky] of block b for every input column (tail columns repeat the last one)
+      {
+        constexpr int NC = (NINX + NW - 1) / NW;
+        const int w0 = fm_win<U, DELTA, NINY>(16 * b);
+        fm_s4 xa[NC];
+        fm_f4 vt[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+          const int x = min(wave + NW * i, NINX - 1);
+          xa[i] = fm_tr_read(in_img + (w0 + 4 * g + tq) * G::IN_PITCH + x * 8 + 2 * tp);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          vt[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa[i]), gmy[b],
+                                                        fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+          const int x = min(wave + NW * i, NINX - 1);
+          *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) = fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
+        }
+      }
+      __syncthreads();
+      if (b == 2 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);  // input image dead: prefetch
+      // ---- horizontal: up (NBX column blocks), activation, down (NOB output blocks) for this wave's rows
+      fm_s4 vb[RR][NBX];
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int tt = 0; tt < NBX; ++tt) {
+          const int w0 = fm_win<U, DELTA, NINX>(16 * tt);
+          vb[rr][tt] = fm_tr_read(v_img + (wave + NW * rr) * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      fm_f4 u[RR][NBX];
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int tt = 0; tt < NBX; ++tt)
+          u[rr][tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[rr][tt]),
+                                                            fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      uint2 au[RR][NBX];
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int tt = 0; tt < NBX; ++tt)
+          au[rr][tt] = fm_act_h4(fm_h2u(u[rr][tt][0], u[rr][tt][1]), fm_h2u(u[rr][tt][2], u[rr][tt][3]), slope2,
+                                 nlim2, lim2);
+      __builtin_amdgcn_sched_barrier(0);
+      fm_f4 d[RR][NOB];
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          d[rr][ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[rr][2 * ob], au[rr][2 * ob + 1]), gdh01,
+                                                             fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          d[rr][ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[rr][2 * ob + 2], make_uint2(0u, 0u)), gdh2,
+                                                             d[rr][ob], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          *reinterpret_cast<uint2*>(d_img + (wave + NW * rr) * G::D_PITCH + (16 * ob + li) * G::D_XP + 2 * g) =
+              fm_pack4(d[rr][ob][0], d[rr][ob][1], d[rr][ob][2], d[rr][ob][3]);
+      __syncthreads();
+      // ---- vertical down: accumulate block b's 16 grid rows into this wave's output columns
+      fm_s4 da[OCW];
+#pragma unroll
+      for (int i = 0; i < OCW; ++i)
+        da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + NW * i) * G::D_XP + 2 * tp);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < OCW; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[b], acc[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox)
+    float ps[4] = {1.f, 1.f, 1.f, 1.f};
+    if (a.post_scale) {
+      const float4 p = *reinterpret_cast<const float4*>(a.post_scale + (int64_t)n * a.c_p + c0 + 4 * g);
+      ps[0] = p.x; ps[1] = p.y; ps[2] = p.z; ps[3] = p.w;
+    }
+    const int gy = oy0 + li;
+#pragma unroll
+    for (int i = 0; i < OCW; ++i) {
+      const int gx = ox0 + wave + NW * i;
+      if (gy < a.out_h && gx < a.out_w) {
+        const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
+                                   (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
+        *reinterpret_cast<uint2*>(yout + (((int64_t)n * a.out_h + gy) * a.out_w + gx) * a.c_p + c0 + 4 * g) = v;
+      }
+    }
+  }
+}
+
+template <int U, int DELTA>
+static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
+  constexpr int TOX = 32, NW = 8;
+  a.tiles_x = (int)ceil_div(a.out_w, TOX);
+  a.tiles_y = (int)ceil_div(a.out_h, 16);
+  a.cblocks = a.c_p / 16;
+  const int ntiles = n * a.tiles_y * a.tiles_x * a.cblocks;
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma2_kernel<U, DELTA, TOX, NW>, 64 * NW, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL((flrelu_mfma2_kernel<U, DELTA, TOX, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, ntiles);
+}
+
 template <int U, int DELTA, bool IN_F16, bool ALIAS, int NW>
 static void fm_launch_alias(const FlrArgs& a, int ntiles, hipStream_t s) {
   // persistent grid: every CU filled to the kernel's occupancy, capped by the tile count
@@ -463,6 +769,26 @@ static void fm_launch(const FlrArgs& a, int up, int delta, int ntiles, hipStream
 int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, int delta, int n, hipStream_t s) {
   if (down != 2 || td != 12 || tu != 6 * up || (up != 2 && up != 4) || a.bias != nullptr || a.c_p % 16 != 0)
     return IC2_E_UNSUPPORTED;
+  if ((int64_t)a.in_h * a.in_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // 32-bit buffer offsets
+  // the wide (16 x 32) tile for the f16-input synthesis path unless IC2_FLR_WIDE=0
+  static const bool wide = [] {
+    const char* e = getenv("IC2_FLR_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (in_f16 && wide && (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {
+    if (up == 2) {
+      if (delta == 0) fm2_launch<2, 0>(a, n, s);
+      else fm2_launch<2, 1>(a, n, s);
+    } else {
+      switch (delta) {
+        case 0: fm2_launch<4, 0>(a, n, s); break;
+        case 1: fm2_launch<4, 1>(a, n, s); break;
+        case 2: fm2_launch<4, 2>(a, n, s); break;
+        default: fm2_launch<4, 3>(a, n, s); break;
+      }
+    }
+    return IC2_OK;
+  }
   a.tiles_x = (int)ceil_div(a.out_w, 16);
   a.tiles_y = (int)ceil_div(a.out_h, 16);
   a.cblocks = a.c_p / 16;

@@ -29,10 +29,11 @@ def child(kind):
         conv = s_in + 2
         s_out = int(L.out_size[0])
         if kind == "flr":
-            y = (torch.randn(n, conv, conv, L.cout_p, device=dev) * 2).to(torch.bfloat16)
+            # f16 input: what the synthesis conv epilogue hands the fused filtered lrelu
+            y = (torch.randn(n, conv, conv, L.cout_p, device=dev) * 2).to(torch.float16)
             out = torch.empty(n, s_out, s_out, L.cout_p, device=dev, dtype=torch.bfloat16)
             def run():
-                nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.BF16, nv.BF16, n, L.cout_p, conv, conv, s_out,
+                nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.F16, nv.BF16, n, L.cout_p, conv, conv, s_out,
                         s_out, L._fu.ctypes.data_as(__import__("ctypes").c_void_p), L._fu.shape[0],
                         L._fd.ctypes.data_as(__import__("ctypes").c_void_p), L._fd.shape[0], None, L.up_factor,
                         L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0, None, nv.stream_of(y))
@@ -62,15 +63,15 @@ def child(kind):
 
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "flr"
-    variants = sys.argv[2:] or ["0"]
-    env_name = "IC2_FLR_VARIANT" if kind == "flr" else "IC2_IGEMM_TILE"
+    variants = sys.argv[2:] or ["default"]
     table = {}
     for v in variants:
-        # "v" or "v,p" (p = IC2_FLR_PERSIST for flr, IC2_IGEMM_GROUP for igemm)
-        parts = v.split(",")
-        env = dict(os.environ, **{env_name: parts[0]})
-        if len(parts) > 1:
-            env["IC2_FLR_PERSIST" if kind == "flr" else "IC2_IGEMM_GROUP"] = parts[1]
+        # each variant: "default" or a comma list of ENV=value overrides (read once per child process)
+        env = dict(os.environ)
+        for kv in v.split(","):
+            if "=" in kv:
+                k, val = kv.split("=")
+                env[k] = val
         r = subprocess.run([sys.executable, __file__, "--child", kind], env=env, capture_output=True, text=True,
                            timeout=600)
         if r.returncode != 0:
@@ -79,7 +80,7 @@ def main():
         table[v] = json.loads(r.stdout.strip().splitlines()[-1])
     names = list(next(iter(table.values())).keys()) if table else []
     print(f"{kind}: us (TFLOP/s) per layer, batch 32 bf16")
-    print(f"{'layer':14s}" + "".join(f"{'v' + v:>16s}" for v in table))
+    print(f"{'layer':14s}" + "".join(f"{v[:15]:>16s}" for v in table))
     for nm in names:
         print(f"{nm:14s}" + "".join(f"{str(table[v][nm]):>16s}" for v in table))
     print(f"{'total us':14s}" + "".join(f"{sum(x[0] for x in table[v].values()):16.1f}" for v in table))
