@@ -775,7 +775,9 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
     const char* e = getenv("IC2_FLR_WIDE");
     return !(e && e[0] == '0');
   }();
-  if (in_f16 && wide && (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {
+  // (only where 32-column tiles pad the output no wider than 16-column ones: not the 36-wide SG3 layers)
+  if (in_f16 && wide && ceil_div(a.out_w, 32) * 32 <= ceil_div(a.out_w, 16) * 16 &&
+      (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {
     if (up == 2) {
       if (delta == 0) fm2_launch<2, 0>(a, n, s);
       else fm2_launch<2, 1>(a, n, s);
