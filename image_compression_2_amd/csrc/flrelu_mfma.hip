@@ -121,6 +121,23 @@ __device__ __forceinline__ uint2 fm_act_h4(uint32_t h0, uint32_t h1, uint32_t sl
   return make_uint2(h0, h1);
 }
 
+// clamp-split activation for a finite clamp (CL kernels): the up pass produces u' = u / lim, and
+//   lrelu(u) clamped to [-lim, lim] = lim * (clamp01(u') - clamp01(-slope * u'))
+// (u >= 0: min(u, lim); u < 0: max(slope * u, -lim)), so after the f16 conversion each pair costs two packed
+// instructions with the hardware [0, 1] clamp; the factor lim and the subtraction go into the down-pass
+// matrices, whose K doubles (positive and negative parts), on the otherwise idle matrix pipe.
+__device__ __forceinline__ void fm_act_split(uint32_t h0, uint32_t h1, uint32_t nslope2, uint2& pos, uint2& neg) {
+  uint32_t p0, p1, n0, n1;
+  asm("v_pk_max_f16 %0, %4, 0 clamp\n\t"
+      "v_pk_max_f16 %1, %5, 0 clamp\n\t"
+      "v_pk_mul_f16 %2, %4, %6 clamp\n\t"
+      "v_pk_mul_f16 %3, %5, %6 clamp"
+      : "=&v"(p0), "=&v"(p1), "=&v"(n0), "=&v"(n1)
+      : "v"(h0), "v"(h1), "v"(nslope2));
+  pos = make_uint2(p0, p1);
+  neg = make_uint2(n0, n1);
+}
+
 __device__ __forceinline__ int fm_xcd_remap(int b, int nblocks) {
   const int xcd = b & 7, loc = b >> 3;
   const int q8 = nblocks >> 3, r8 = nblocks & 7;
@@ -461,8 +478,8 @@ struct FmGeom2 {
   static_assert(NBX == 2 * NOB + 1, "horizontal down: output block ob reads grid blocks 2ob .. 2ob+2");
 };
 
-template <int U, int DELTA, int TOX, int NW>
-__global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int ntiles) {
+template <int U, int DELTA, int TOX, int NW, bool CL>
+__global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs a, int ntiles) {  // 2 WGs / CU
   constexpr int NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;  // grid rows per wave per block; output columns per wave
   using G = FmGeom2<U, TOX>;
   constexpr int NINY = G::NINY, NINX = G::NINX, NBX = G::NBX, NOB = G::NOB, NCH = G::NCH;
@@ -544,26 +561,40 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int nt
     for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
     gmy[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
+  const float inv_lim = CL ? 1.f / a.lim : 1.f;  // CL: the horizontal up pass yields u / lim
 #pragma unroll
   for (int t = 0; t < NBX; ++t) {
     const int w0 = fm_win<U, DELTA, NINX>(16 * t);
     float v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
+    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)] * inv_lim;
     gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
-  fm_h8 gdh01, gdh2;
+  // horizontal down matrices over kx blocks (K = 32 per MFMA).  Plain: [b0; b1], [b2; 0].  CL: taps * lim,
+  // [b0; b1], [b2; -b0], [-b1; -b2] against (pos0, pos1), (pos2, neg0), (neg1, neg2)
+  fm_h8 gdh01, gdh2, gdh3;
   {
+    const float sc = CL ? a.lim : 1.f;
+    auto tap = [&](int blk, int j) { return taps[228 + 16 * blk + 4 * g + j - 2 * li] * sc; };
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kx = (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
-      v[j] = taps[228 + kx - 2 * li];
+    for (int j = 0; j < 4; ++j) {
+      v[j] = tap(0, j);
+      v[4 + j] = tap(1, j);
     }
     gdh01 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = taps[228 + 32 + 4 * g + j - 2 * li];
-    gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), make_uint2(0u, 0u));
+    for (int j = 0; j < 4; ++j) {
+      v[j] = tap(2, j);
+      v[4 + j] = CL ? -tap(0, j) : 0.f;
+    }
+    gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = -tap(1, j);
+      v[4 + j] = -tap(2, j);
+    }
+    gdh3 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
   }
   fm_h4 gdv[3];
 #pragma unroll
@@ -573,8 +604,9 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int nt
     for (int j = 0; j < 4; ++j) v[j] = taps[148 + 16 * b + 4 * g + j - 2 * li];
     gdv[b] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
-  const float slope = a.slope, lim = a.lim;
+  const float slope = a.slope, lim = CL ? 1.f : a.lim;
   const uint32_t slope2 = fm_h2u(slope, slope), lim2 = fm_h2u(lim, lim), nlim2 = fm_h2u(-lim, -lim);
+  const uint32_t nslope2 = fm_h2u(-slope, -slope);
   bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
   __syncthreads();  // every wave's tap reads are done before the first D store overwrites the table
 
@@ -615,52 +647,52 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int nt
       }
       __syncthreads();
       if (b == 2 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);  // input image dead: prefetch
-      // ---- horizontal: up (NBX column blocks), activation, down (NOB output blocks) for this wave's rows
-      fm_s4 vb[RR][NBX];
+      // ---- horizontal: up (NBX column blocks), activation, down (NOB output blocks), one grid row of this
+      // wave at a time (bounded register pressure: 2 workgroups per CU need <= 128 VGPRs)
 #pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
+      for (int rr = 0; rr < RR; ++rr) {
+        const int row = wave + NW * rr;
+        fm_s4 vb[NBX];
 #pragma unroll
         for (int tt = 0; tt < NBX; ++tt) {
           const int w0 = fm_win<U, DELTA, NINX>(16 * tt);
-          vb[rr][tt] = fm_tr_read(v_img + (wave + NW * rr) * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
+          vb[tt] = fm_tr_read(v_img + row * G::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
         }
-      __builtin_amdgcn_sched_barrier(0);
-      fm_f4 u[RR][NBX];
-#pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
+        __builtin_amdgcn_sched_barrier(0);
+        fm_f4 u[NBX];
 #pragma unroll
         for (int tt = 0; tt < NBX; ++tt)
-          u[rr][tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[rr][tt]),
-                                                            fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      uint2 au[RR][NBX];
+          u[tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[tt]),
+                                                        fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        uint2 au[NBX], an[NBX];
 #pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
-#pragma unroll
-        for (int tt = 0; tt < NBX; ++tt)
-          au[rr][tt] = fm_act_h4(fm_h2u(u[rr][tt][0], u[rr][tt][1]), fm_h2u(u[rr][tt][2], u[rr][tt][3]), slope2,
-                                 nlim2, lim2);
-      __builtin_amdgcn_sched_barrier(0);
-      fm_f4 d[RR][NOB];
-#pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
+        for (int tt = 0; tt < NBX; ++tt) {
+          const uint32_t h0 = fm_h2u(u[tt][0], u[tt][1]), h1 = fm_h2u(u[tt][2], u[tt][3]);
+          if constexpr (CL) fm_act_split(h0, h1, nslope2, au[tt], an[tt]);
+          else au[tt] = fm_act_h4(h0, h1, slope2, nlim2, lim2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        fm_f4 d[NOB];
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob)
-          d[rr][ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[rr][2 * ob], au[rr][2 * ob + 1]), gdh01,
-                                                             fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
+          d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob], au[2 * ob + 1]), gdh01,
+                                                         fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob)
-          d[rr][ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[rr][2 * ob + 2], make_uint2(0u, 0u)), gdh2,
-                                                             d[rr][ob], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+          d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob + 2], CL ? an[2 * ob] : make_uint2(0u, 0u)),
+                                                         gdh2, d[ob], 0, 0, 0);
+        if constexpr (CL) {
 #pragma unroll
-      for (int rr = 0; rr < RR; ++rr)
+          for (int ob = 0; ob < NOB; ++ob)
+            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(an[2 * ob + 1], an[2 * ob + 2]), gdh3, d[ob], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob)
-          *reinterpret_cast<uint2*>(d_img + (wave + NW * rr) * G::D_PITCH + (16 * ob + li) * G::D_XP + 2 * g) =
-              fm_pack4(d[rr][ob][0], d[rr][ob][1], d[rr][ob][2], d[rr][ob][3]);
+          *reinterpret_cast<uint2*>(d_img + row * G::D_PITCH + (16 * ob + li) * G::D_XP + 2 * g) =
+              fm_pack4(d[ob][0], d[ob][1], d[ob][2], d[ob][3]);
+      }
       __syncthreads();
       // ---- vertical down: accumulate block b's 16 grid rows into this wave's output columns
       fm_s4 da[OCW];
@@ -693,8 +725,8 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma2_kernel(FlrArgs a, int nt
   }
 }
 
-template <int U, int DELTA>
-static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
+template <int U, int DELTA, bool CL>
+static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
   constexpr int TOX = 32, NW = 8;
   a.tiles_x = (int)ceil_div(a.out_w, TOX);
   a.tiles_y = (int)ceil_div(a.out_h, 16);
@@ -705,11 +737,23 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma2_kernel<U, DELTA, TOX, NW>, 64 * NW, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL>, 64 * NW, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((flrelu_mfma2_kernel<U, DELTA, TOX, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, ntiles);
+  hipLaunchKernelGGL((flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, ntiles);
+}
+
+// the clamp-split activation needs a finite clamp whose reciprocal scaling keeps the f16 operands normal
+// (lim in [2^-4, 2^12]: SG3's conv_clamp 256 / sqrt(2)); IC2_FLR_CLSPLIT=0 keeps the 3-instruction activation
+template <int U, int DELTA>
+static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
+  static const bool split = [] {
+    const char* e = getenv("IC2_FLR_CLSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (split && a.lim >= 0.0625f && a.lim <= 4096.f) fm2_launch_cl<U, DELTA, true>(a, n, s);
+  else fm2_launch_cl<U, DELTA, false>(a, n, s);
 }
 
 template <int U, int DELTA, bool IN_F16, bool ALIAS, int NW>

@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -k "flrelu or fi
 rc=$?
 tail -15 gpurun_out/flr_tests.log
 [ $rc -eq 0 ] || { echo "flr tests failed ($rc): stopping"; exit $rc; }
-timeout -k 10 600 python tools/bench_kernels.py flr default IC2_FLR_WIDE=0 2>&1 | tee gpurun_out/flr_layers.txt
+timeout -k 10 600 python tools/bench_kernels.py flr default IC2_FLR_CLSPLIT=0 IC2_FLR_WIDE=0 2>&1 | tee gpurun_out/flr_layers.txt
 [ ${PIPESTATUS[0]} -eq 0 ] || exit 1
 timeout -k 10 600 python -u -m pytest tests/test_gpu_c2_parity.py -q -s -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/c2_parity.log 2>&1
 rc=$?
