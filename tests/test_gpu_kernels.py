@@ -227,6 +227,62 @@ def test_flrelu_nhwc_bf16_matches_oracle(cuda, gen256_bf16_layers, layer, c_p, i
     assert err.mean().item() < 2e-3 * (1 + r.abs().mean().item())
 
 
+def test_f16_saturation_semantics(cuda, gen256_bf16_layers):
+    """bf16 mode hands the filtered lrelu the modulated-conv output as f16 (its MFMA operand type), so a
+    pre-activation beyond +-65504 saturates BEFORE the up-FIR, while the reference's fp32 CPU path clamps (at
+    conv_clamp 256) only AFTER it; SG3's own CUDA path has the same f16 range in its fp16 layers.  Pinned:
+    (1) the conv epilogue saturates to exactly +-65504 (no inf / NaN reaches the FIR); (2) the filtered lrelu of
+    the saturated tensor equals the oracle on that tensor; (3) against the unsaturated oracle the outputs differ
+    only inside the FIR support of a saturated pixel (DESIGN.md (c) records the measured deviation)."""
+    import ctypes
+    # (1) conv epilogue, f16 output
+    g = torch.Generator().manual_seed(90)
+    x = torch.randn(1, 8, 8, 32, generator=g).to(torch.bfloat16)
+    x[0, 3, 3, :] = 3000.0
+    w = (torch.randn(32, 1, 1, 32, generator=g) * 8).to(torch.bfloat16)
+    y = torch.empty(1, 8, 8, 32, device=cuda, dtype=torch.float16)
+    xd, wd = x.to(cuda), w.to(cuda)
+    nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), nv.BF16, nv.F16, 1, 8, 8, 32, 32, 32, 1, 1, 0, 8, 8, None, None,
+                  0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(xd), cuda)
+    torch.cuda.synchronize()
+    ref = torch.einsum("nhwc,oc->nhwo", x.double(), w.double()[:, 0, 0])
+    assert torch.isfinite(y).all() and (ref.abs() > 65504).any()
+    assert torch.equal(y.cpu().double()[ref.abs() > 65520], ref.clamp(-65504, 65504)[ref.abs() > 65520])
+    # (2) + (3) filtered lrelu of a tensor with saturated pixels (SG3-T-256 L8 geometry)
+    L = gen256_bf16_layers[8]
+    n, c_p, conv, s_out = 1, 32, int(L.in_size[0]) + 2, int(L.out_size[0])
+    xr = torch.randn(n, c_p, conv, conv, generator=g) * 2
+    hot = [(20, 30), (75, 75), (140, 9)]
+    for (py, px) in hot:
+        xr[:, :, py, px] = 2.0e5 * torch.sign(torch.randn(c_p, generator=g))[None, :]
+    xs = xr.clamp(-65504, 65504).to(torch.float16).float()
+    xd = xs.permute(0, 2, 3, 1).contiguous().to(cuda, torch.float16)
+    out = torch.empty(n, s_out, s_out, c_p, device=cuda, dtype=torch.bfloat16)
+    nv.call("ic2_flrelu_nhwc", nv.ptr(xd), nv.ptr(out), nv.F16, nv.BF16, n, c_p, conv, conv, s_out, s_out,
+            L._fu.ctypes.data_as(ctypes.c_void_p), L._fu.shape[0], L._fd.ctypes.data_as(ctypes.c_void_p),
+            L._fd.shape[0], None, L.up_factor, L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0, None,
+            nv.stream_of(xd))
+    torch.cuda.synchronize()
+    kw = dict(up=L.up_factor, down=L.down_factor, padding=L.padding, gain=np.sqrt(2), slope=0.2, clamp=256.0)
+    fu, fd = torch.from_numpy(L._fu).double(), torch.from_numpy(L._fd).double()
+    r_sat = sg3.filtered_lrelu(xs.double(), fu, fd, None, **kw)
+    yv = out.float().cpu().permute(0, 3, 1, 2).double()
+    assert (yv - r_sat).abs().max().item() < 2e-2 * (1 + r_sat.abs().max().item())
+    # the saturation alone (f32 elsewhere) against the unsaturated reference
+    r_raw = sg3.filtered_lrelu(xr.double(), fu, fd, None, **kw)
+    r_clp = sg3.filtered_lrelu(xr.clamp(-65504, 65504).double(), fu, fd, None, **kw)
+    # outputs whose input support holds no saturated pixel are unaffected by the saturation
+    near = torch.zeros(s_out, s_out, dtype=torch.bool)
+    rad = (L.up_taps // L.up_factor + L.down_taps) // 2 + 2
+    for (py, px) in hot:
+        cy, cx = (py * L.up_factor + L.padding[2]) // L.down_factor, (px * L.up_factor + L.padding[0]) // L.down_factor
+        near[max(cy - rad, 0):cy + rad + 1, max(cx - rad, 0):cx + rad + 1] = True
+    dev = (r_raw - r_clp).abs()
+    assert dev[..., ~near].max().item() == 0.0
+    print(f"[f16-saturation] max |raw - saturated| inside the support of 3 saturated pixels: "
+          f"{dev[..., near].max().item():.3f} (outputs clamp at 256)")
+
+
 # ------------------------------------------------------------------ implicit-GEMM conv (MFMA)
 IGEMM_CASES = [(3, 32, 19, 1, 0), (64, 96, 12, 1, 0), (181, 128, 9, 2, 0), (512, 512, 6, 2, 0),
                (256, 362, 10, 2, 1), (96, 64, 13, 1, 2), (128, 181, 11, 2, 3), (512, 256, 7, 2, 4),
