@@ -60,9 +60,16 @@ _SIGS = {
     "ic2_rc_bound": [_I64, _I64],
     "ic2_rc_encode": [_P, _I64, _I, _I, _I, _P, _I64, _P, _I],
     "ic2_rc_decode": [_P, _P, _I64, _I, _I, _I, _P, _I],
+    "ic2_conv_wgrad_ws_floats": [_I, _I, _I, _I, _I, _I, _I, _I],
+    "ic2_conv_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I64, _P],
+    "ic2_gn_lrelu_pool_bwd_floats": [_I, _I, _I, _I, _I],
+    "ic2_gn_lrelu_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _I64,
+                              _P],
+    "ic2_gap_bwd": [_P, _P, _I, _I, _I, _I, _I, _P],
 }
 _RESTYPE = {"ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
-            "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64}
+            "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64, "ic2_conv_wgrad_ws_floats": _I64,
+            "ic2_gn_lrelu_pool_bwd_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()

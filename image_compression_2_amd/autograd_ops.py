@@ -1,0 +1,170 @@
+"""Autograd wrappers over the HIP kernels: the training path of the reference (BASELINE config C5,
+``train_hvae_encoder``, /root/reference/stylegan3_hvae_full.py:655-707) backpropagates through
+HVAE_VGG_Encoder (loss.backward at :693-696).  Each op's forward is the inference kernel; its backward is a
+HIP kernel as well (csrc/backward.hip, or the forward implicit GEMM on transformed weights):
+
+    conv3x3 (nn.Conv2d, :62, :175-176)   fwd ic2_conv_igemm         bwd dx: ic2_conv_igemm on flipped, transposed
+                                                                     weights; dW: ic2_conv_wgrad; db: column sum
+    GroupNorm -> lrelu (-> AvgPool2d)    fwd ic2_group_norm_stats +  bwd ic2_gn_lrelu_pool_bwd
+    (:183-191)                               ic2_gn_lrelu_pool
+    AdaptiveAvgPool2d(1) (:218)          fwd ic2_global_avg_pool    bwd ic2_gap_bwd
+    NCHW -> NHWC input packing           fwd ic2_nchw_to_nhwc       bwd ic2_nhwc_to_nchw
+
+Activations are NHWC with padded channel strides, in the module's precision (f32 parity mode / bf16);
+gradients flow in the same layout and dtype; weight gradients are f32.  The projector MLPs are [N, <=512]
+matrices and run as torch ops on the device.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nv
+
+
+def _pad_to(c_p, t):
+    return t if t.shape[-1] == c_p else torch.nn.functional.pad(t, (0, c_p - t.shape[-1]))
+
+
+def pack_conv_weight(weight, cin_p, cout_p, dt):
+    """[cout][cin][kh][kw] f32 -> packed [cout_p][kh][kw][cin_p] (dt) on the device."""
+    w = weight.detach().to(torch.float32).contiguous()
+    cout, cin, kh, kw = w.shape
+    out = torch.empty([cout_p, kh, kw, cin_p], dtype=dt, device=w.device)
+    nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(out), nv.dtype_code(dt),
+            None, nv.stream_of(w))
+    return out
+
+
+def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None):
+    n, h, w, cin_p = x.shape
+    cout_p = wp.shape[0]
+    ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kh + 1
+    dt_out = x.dtype if dt_out is None else dt_out
+    y = torch.empty([n, ho, wo, cout_p], dtype=dt_out, device=x.device)
+    nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.dtype), nv.dtype_code(dt_out), n, h, w, cin_p,
+                  cout_p, cout_valid, kh, kh, pad, ho, wo, None, nv.ptr(bias_p), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
+                  nv.stream_of(x), x.device)
+    return y
+
+
+class Conv2dNHWC(torch.autograd.Function):
+    """nn.Conv2d (stride 1, zero padding, k x k) on NHWC activations with padded channel strides."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, pad, cout_p):
+        cout, cin, kh, kw = weight.shape
+        cin_p = x.shape[-1]
+        wp = pack_conv_weight(weight, cin_p, cout_p, x.dtype)
+        bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
+        if bias is not None:
+            bp[:cout] = bias.detach().float()
+        y = conv_nhwc(x, wp, bp, cout, kh, pad)
+        ctx.save_for_backward(x, weight)
+        ctx.pad, ctx.has_bias = pad, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        cout, cin, kh, kw = weight.shape
+        n, h, w, cin_p = x.shape
+        dy = dy.to(x.dtype).contiguous()
+        cout_p = dy.shape[-1]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # dx = conv(dy, W flipped in space, transposed in channels), padding k - 1 - pad
+            wt = weight.detach().transpose(0, 1).flip(2, 3)
+            wtp = pack_conv_weight(wt, cout_p, cin_p, x.dtype)
+            dx = conv_nhwc(dy, wtp, None, cin_p, kh, kh - 1 - ctx.pad)
+        if ctx.needs_input_grad[1]:
+            nfl = int(nv.query("ic2_conv_wgrad_ws_floats", n, h, w, cin_p, cout_p, kh, kw, ctx.pad))
+            ws = torch.empty([max(nfl, 4)], dtype=torch.float32, device=x.device)
+            dwp = torch.empty([cout_p, kh, kw, cin_p], dtype=torch.float32, device=x.device)
+            nv.call("ic2_conv_wgrad", nv.ptr(x), nv.ptr(dy), nv.ptr(dwp), nv.dtype_code(x.dtype), n, h, w, cin_p,
+                    cout_p, kh, kw, ctx.pad, nv.ptr(ws), nfl, nv.stream_of(x))
+            dw = dwp[:cout, :, :, :cin].permute(0, 3, 1, 2).contiguous()
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, cout_p)[:, :cout].float().sum(0)
+        return dx, dw, db, None, None
+
+
+class GroupNormLReluPoolNHWC(torch.autograd.Function):
+    """nn.GroupNorm(groups, c, eps) -> F.leaky_relu(slope) (-> nn.AvgPool2d(2, 2)) on NHWC."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, groups, eps, slope, pool, c, dt_out):
+        n, h, w, c_p = y.shape
+        stream = nv.stream_of(y)
+        nfl = int(nv.query("ic2_group_norm_stats_floats", n, h * w, groups))
+        stats = torch.empty([nfl], dtype=torch.float32, device=y.device)
+        nv.call("ic2_group_norm_stats", nv.ptr(y), nv.dtype_code(y.dtype), n, h * w, c_p, c, groups, float(eps),
+                nv.ptr(stats), stream)
+        oh, ow = (h // 2, w // 2) if pool else (h, w)
+        out = torch.empty([n, oh, ow, c_p], dtype=dt_out, device=y.device)
+        g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+        nv.call("ic2_gn_lrelu_pool", nv.ptr(y), nv.ptr(out), nv.dtype_code(y.dtype), nv.dtype_code(dt_out), n, h, w,
+                c_p, c, groups, nv.ptr(stats), nv.ptr(g32), nv.ptr(b32), float(slope), int(pool), stream)
+        ctx.save_for_backward(y, stats, g32, b32)
+        ctx.meta = (groups, slope, pool, c)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, stats, g32, b32 = ctx.saved_tensors
+        groups, slope, pool, c = ctx.meta
+        n, h, w, c_p = y.shape
+        dout = dout.contiguous()
+        nfl = int(nv.query("ic2_gn_lrelu_pool_bwd_floats", n, h, w, c_p, groups))
+        ws = torch.empty([nfl], dtype=torch.float32, device=y.device)
+        dy = torch.empty_like(y)
+        dgamma = torch.empty([c], dtype=torch.float32, device=y.device)
+        dbeta = torch.empty([c], dtype=torch.float32, device=y.device)
+        nv.call("ic2_gn_lrelu_pool_bwd", nv.ptr(y), nv.ptr(dout), nv.ptr(dy), nv.dtype_code(y.dtype),
+                nv.dtype_code(dout.dtype), nv.dtype_code(dy.dtype), n, h, w, c_p, c, groups, nv.ptr(stats),
+                nv.ptr(g32), nv.ptr(b32), float(slope), int(pool), nv.ptr(dgamma), nv.ptr(dbeta), nv.ptr(ws), nfl,
+                nv.stream_of(y))
+        return dy, dgamma, dbeta, None, None, None, None, None, None
+
+
+class GlobalAvgPoolNHWC(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) + flatten: NHWC [n, h, w, c_p] -> [n, c] f32."""
+
+    @staticmethod
+    def forward(ctx, x, c):
+        n, h, w, c_p = x.shape
+        nfl = int(nv.query("ic2_global_avg_pool_floats", n, h * w, c_p, c))
+        buf = torch.empty([nfl], dtype=torch.float32, device=x.device)
+        nv.call("ic2_global_avg_pool", nv.ptr(x), nv.dtype_code(x.dtype), n, h * w, c_p, c, nv.ptr(buf),
+                nv.stream_of(x))
+        ctx.shape, ctx.dtype, ctx.c = x.shape, x.dtype, c
+        return buf[: n * c].view(n, c).clone()
+
+    @staticmethod
+    def backward(ctx, dp):
+        n, h, w, c_p = ctx.shape
+        dp = dp.float().contiguous()
+        dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=dp.device)
+        nv.call("ic2_gap_bwd", nv.ptr(dp), nv.ptr(dx), nv.dtype_code(ctx.dtype), n, h * w, c_p, ctx.c,
+                nv.stream_of(dp))
+        return dx, None
+
+
+class ToNHWC(torch.autograd.Function):
+    """NCHW f32 -> NHWC (dt, channel stride c_p, zero-padded)."""
+
+    @staticmethod
+    def forward(ctx, x, dt, c_p):
+        n, c, h, w = x.shape
+        out = torch.empty([n, h, w, c_p], dtype=dt, device=x.device)
+        nv.call("ic2_nchw_to_nhwc", nv.ptr(x), nv.ptr(out), nv.dtype_code(dt), n, c, h, w, c_p, None, nv.stream_of(x))
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty([n, c, h, w], dtype=torch.float32, device=dy.device)
+        nv.call("ic2_nhwc_to_nchw", nv.ptr(dy), nv.dtype_code(dy.dtype), nv.ptr(dx), n, c, h, w, dy.shape[-1],
+                nv.stream_of(dy))
+        return dx, None, None

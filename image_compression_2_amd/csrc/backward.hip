@@ -1,0 +1,450 @@
+// Backward kernels of the training path (BASELINE config C5): the reference trains
+// HVAE_VGG_Encoder through torch autograd (stylegan3_hvae_full.py:655-707: recon / KL losses, backward at
+// :693-696).  The encoder's hot ops get hand-written backward kernels here; the 3x3 conv's input gradient
+// is the forward implicit GEMM on flipped / transposed weights (ic2_conv_igemm), so only the weight
+// gradient and the GroupNorm + lrelu + avg-pool backward are new.
+//
+//   ic2_conv_wgrad : dW[o][ky][kx][i] = sum_p dy[p][o] * x[p shifted by (ky, kx)][i]  (MFMA; K = pixels)
+//   ic2_gn_lrelu_pool_bwd : d(AvgPool2(lrelu(GroupNorm(y)))) / dy, dgamma, dbeta
+//   ic2_gap_bwd : d(mean over H x W) / dx  (the HierarchyProjector's AdaptiveAvgPool2d(1))
+#include "common.h"
+
+namespace ic2 {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 wg_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float wg_f32x4;
+typedef short wg_s4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient as a GEMM over pixels: C[o][j] (j = one tap's 64 input channels) = sum_p A[o][p] B[p][j],
+// A = dy^T, B = the tap-shifted input.  Both operands are pixel-major in HBM (NHWC), so a 32-pixel chunk of
+// each is staged row-per-pixel in LDS and the MFMA fragments (8 consecutive pixels of one column) are read
+// with the transposing ds_read_b64_tr_b16 (two per fragment).  Tile 64 (o) x 64 (j) x 32 (p), 4 waves of
+// 32 x 32; the pixels are split over gridDim.y into f32 partial slabs summed in slice order by
+// wgrad_reduce_kernel (deterministic).  f32 operands: 16x16x4 f32 MFMAs on plain LDS reads.
+constexpr int WG_BO = 64, WG_BJ = 64, WG_KP = 32;
+constexpr int WG_PITCH = WG_BO + 8;  // LDS row pitch (elements)
+
+struct WgradArgs {
+  const void* x;
+  const void* dy;
+  float* part;  // [splits][cout_p][kh*kw][cin_p]
+  int n, h, w, cin_p, cout_p, kh, kw, pad, ho, wo;
+  int P;        // n * ho * wo
+  int chunks;   // ceil(P / 32)
+  int j_tiles;  // kh * kw * cin_p / 64
+};
+
+template <typename T>
+__device__ __forceinline__ void wg_load_row(const T* src, bool ok, T* dst);
+
+template <>
+__device__ __forceinline__ void wg_load_row<bf16_t>(const bf16_t* src, bool ok, bf16_t* dst) {
+  const uint4 v = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0u, 0u, 0u, 0u);
+  *reinterpret_cast<uint4*>(dst) = v;  // 8 elements
+}
+template <>
+__device__ __forceinline__ void wg_load_row<float>(const float* src, bool ok, float* dst) {
+  const float4 a = ok ? reinterpret_cast<const float4*>(src)[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 b = ok ? reinterpret_cast<const float4*>(src)[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+  reinterpret_cast<float4*>(dst)[0] = a;
+  reinterpret_cast<float4*>(dst)[1] = b;
+}
+
+__device__ __forceinline__ wg_s4 wg_tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) wg_s4*)p);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) T sdy[WG_KP * WG_PITCH];
+  __shared__ __attribute__((aligned(16))) T sx[WG_KP * WG_PITCH];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int o_tiles = (a.cout_p + WG_BO - 1) / WG_BO;  // channel strides are multiples of 32: a 32-wide tail
+  const int o0 = (blockIdx.x % o_tiles) * WG_BO;       // tile reads zeros and stores nothing past the stride
+  const int jt = blockIdx.x / o_tiles;                 // j tile: tap = jt / ceil(cin_p/64), ci block
+  const int cib = (a.cin_p + WG_BJ - 1) / WG_BJ;
+  const int tap = jt / cib, ci0 = (jt - tap * cib) * WG_BJ;
+  const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+  const int c0 = (int)((int64_t)a.chunks * blockIdx.y / gridDim.y);
+  const int c1 = (int)((int64_t)a.chunks * (blockIdx.y + 1) / gridDim.y);
+  const int wo_ = wave >> 1, wj_ = wave & 1;           // this wave's 32 x 32 sub-tile
+  const T* dyg = reinterpret_cast<const T*>(a.dy);
+  const T* xg = reinterpret_cast<const T*>(a.x);
+  // staging: thread -> (pixel row r = tid / 8, 8-element segment s = tid % 8) of each operand
+  const int r = tid >> 3, seg = tid & 7;
+  const int hwo = a.ho * a.wo;
+
+  wg_f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = c0; ch < c1; ++ch) {
+    const int p = ch * WG_KP + r;
+    const bool okp = p < a.P;
+    const int pp = okp ? p : 0;
+    const int nn = pp / hwo;
+    const int rem = pp - nn * hwo;
+    const int oy = rem / a.wo, ox = rem - (rem / a.wo) * a.wo;
+    const int iy = oy - a.pad + ky, ix = ox - a.pad + kx;
+    const bool okx = okp && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    __syncthreads();  // previous chunk's fragment reads done
+    const bool oko = okp && o0 + seg * 8 < a.cout_p, oki = okx && ci0 + seg * 8 < a.cin_p;
+    wg_load_row<T>(dyg + (int64_t)pp * a.cout_p + (oko ? o0 + seg * 8 : 0), oko, sdy + r * WG_PITCH + seg * 8);
+    wg_load_row<T>(xg + (((int64_t)nn * a.h + (okx ? iy : 0)) * a.w + (okx ? ix : 0)) * a.cin_p + (oki ? ci0 + seg * 8 : 0),
+                   oki, sx + r * WG_PITCH + seg * 8);
+    __syncthreads();
+    if constexpr (sizeof(T) == 2) {
+      // A[m = o][k = p]: lane (g, li) = pixels 8g .. 8g+7 of column o; two transposed reads of 4 rows each.
+      // Within a 16-lane group, lane (tq = li / 4, tp = li % 4) reads row base + tq, elements 4 tp .. 4 tp + 3.
+      const int tq = li >> 2, tp = li & 3;
+      wg_bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wo_ * 32 + i * 16 + 4 * tp;
+        const wg_s4 lo = wg_tr_read(reinterpret_cast<const bf16_t*>(sdy) + (8 * g + tq) * WG_PITCH + col);
+        const wg_s4 hi = wg_tr_read(reinterpret_cast<const bf16_t*>(sdy) + (8 * g + 4 + tq) * WG_PITCH + col);
+        af[i] = __builtin_bit_cast(wg_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wj_ * 32 + j * 16 + 4 * tp;
+        const wg_s4 lo = wg_tr_read(reinterpret_cast<const bf16_t*>(sx) + (8 * g + tq) * WG_PITCH + col);
+        const wg_s4 hi = wg_tr_read(reinterpret_cast<const bf16_t*>(sx) + (8 * g + 4 + tq) * WG_PITCH + col);
+        bfr[j] = __builtin_bit_cast(wg_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      // f32: 16x16x4 MFMA, lane (g, li) holds A[m = li][k = g] / B[k = g][n = li] per 4-pixel step (exact fp32)
+      const float* fdy = reinterpret_cast<const float*>(sdy);
+      const float* fx = reinterpret_cast<const float*>(sx);
+#pragma unroll
+      for (int s = 0; s < WG_KP / 4; ++s) {
+        float av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = fdy[(4 * s + g) * WG_PITCH + wo_ * 32 + i * 16 + li];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = fx[(4 * s + g) * WG_PITCH + wj_ * 32 + j * 16 + li];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // C[o = o0 + 32 wo + 16 i + 4 g + rr][j = ci0 + 32 wj + 16 jj + li] -> part[split][o][tap][ci]
+  const int K = a.kh * a.kw * a.cin_p;
+  float* dst = a.part + (int64_t)blockIdx.y * a.cout_p * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int o = o0 + wo_ * 32 + i * 16 + 4 * g + rr;
+        const int ci = ci0 + wj_ * 32 + j * 16 + li;
+        if (o < a.cout_p && ci < a.cin_p) dst[(int64_t)o * K + tap * a.cin_p + ci] = acc[i][j][rr];
+      }
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                           int64_t total, int splits) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    float s = part[e];
+    for (int k = 1; k < splits; ++k) s += part[(int64_t)k * total + e];
+    dw[e] = s;
+  }
+}
+
+static int wgrad_splits(const WgradArgs& a) {
+  const int64_t tiles = ceil_div(a.cout_p, WG_BO) * a.j_tiles;
+  int64_t sp = ceil_div(2048, tiles);
+  if (sp > a.chunks) sp = a.chunks;
+  if (sp > 64) sp = 64;
+  return (int)(sp < 1 ? 1 : sp);
+}
+
+// ------------------------------------------------------------------------------------------------
+// GroupNorm + lrelu (+ 2x2 avg-pool) backward.  Forward (ic2_group_norm_stats + ic2_gn_lrelu_pool):
+//   xhat = (y - mean[n,g]) rstd[n,g],  z = gamma xhat + beta,  a = lrelu(z),  out = pool ? avgpool2(a) : a.
+// Given dout: da = pool ? dout[h/2, w/2] / 4 (0 on a floor-dropped odd row / column) : dout;
+//   dz = da (z > 0 ? 1 : slope);  A[n,c] = sum_hw dz,  B[n,c] = sum_hw dz xhat;
+//   dbeta = sum_n A,  dgamma = sum_n B,  S1[n,g] = sum_{c in g} gamma A,  S2 = sum_{c in g} gamma B,
+//   dy = rstd (gamma dz - S1 / Ng - xhat S2 / Ng),  Ng = H W C / groups.
+// Pass 1: per (n, pixel chunk) per-channel partial sums; pass 2: per (n, c) ordered sum over chunks (f64)
+// -> A, B; pass 3: per (n, g) S1, S2 and per c dbeta, dgamma; pass 4: elementwise dy.  Deterministic.
+constexpr int GNB_CHUNK = 256;  // pixels per pass-1 workgroup
+
+template <typename T> __device__ __forceinline__ float gld(const T* p, int64_t i) { return ld(p + i); }
+
+__device__ __forceinline__ float gnb_dz(float yv, float da, float mean, float rstd, float gam, float bet, float slope,
+                                        float& xhat) {
+  xhat = (yv - mean) * rstd;
+  const float z = gam * xhat + bet;
+  return z > 0.f ? da : da * slope;
+}
+
+template <typename TY, typename TD>
+__device__ __forceinline__ float gnb_da(const TD* dout, int nn, int yy, int xx, int h, int w, int c_p, int cc, int pool) {
+  if (!pool) return gld(dout, (((int64_t)nn * h + yy) * w + xx) * c_p + cc);
+  const int oh = h / 2, ow = w / 2;
+  if (yy >= 2 * oh || xx >= 2 * ow) return 0.f;
+  return 0.25f * gld(dout, (((int64_t)nn * oh + yy / 2) * ow + xx / 2) * c_p + cc);
+}
+
+template <typename TY, typename TD>
+__global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__ y, const TD* __restrict__ dout, int n,
+                                                          int h, int w, int c_p, int c, int groups,
+                                                          const float* __restrict__ stats,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float slope, int pool,
+                                                          int nchunks, float* __restrict__ part) {
+  // thread -> channel cc = t % CT (+ CT steps), pixel phase t / CT
+  __shared__ float sA[256], sB[256];
+  const int hw = h * w;
+  const int chunk = blockIdx.x % nchunks, nn = blockIdx.x / nchunks;
+  const int p0 = chunk * GNB_CHUNK, p1 = min(hw, p0 + GNB_CHUNK);
+  const int CT = c_p < 256 ? c_p : 256, PS = 256 / CT;
+  const int cpg = c / groups;
+  const int cl = threadIdx.x % CT, ph = threadIdx.x / CT;
+  for (int cb = 0; cb < c_p; cb += CT) {
+    const int cc = cb + cl;
+    float sa = 0.f, sb = 0.f;
+    if (ph < PS && cc < c) {
+      const int gi = cc / cpg;
+      const float mean = stats[(nn * groups + gi) * 2], rstd = stats[(nn * groups + gi) * 2 + 1];
+      const float gam = gamma[cc], bet = beta[cc];
+      for (int p = p0 + ph; p < p1; p += PS) {
+        const int yy = p / w, xx = p - (p / w) * w;
+        float xhat;
+        const float dz = gnb_dz(gld(y, ((int64_t)nn * hw + p) * c_p + cc),
+                                gnb_da<TY, TD>(dout, nn, yy, xx, h, w, c_p, cc, pool), mean, rstd, gam, bet, slope, xhat);
+        sa += dz;
+        sb += dz * xhat;
+      }
+    }
+    __syncthreads();
+    sA[threadIdx.x] = sa;
+    sB[threadIdx.x] = sb;
+    __syncthreads();
+    if (ph == 0 && cc < c_p) {
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < PS; ++k) {
+        a += sA[k * CT + cl];
+        b += sB[k * CT + cl];
+      }
+      float* o = part + (((int64_t)nn * c_p + cc) * nchunks + chunk) * 2;
+      o[0] = a;
+      o[1] = b;
+    }
+  }
+}
+
+// per (n, c): ordered f64 sum over the chunks -> AB[n][c][2]
+__global__ void __launch_bounds__(256) gnb_chunks_kernel(const float* __restrict__ part, int nc, int nchunks,
+                                                         double* __restrict__ ab) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc) return;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    a += part[((int64_t)i * nchunks + k) * 2];
+    b += part[((int64_t)i * nchunks + k) * 2 + 1];
+  }
+  ab[2 * i] = a;
+  ab[2 * i + 1] = b;
+}
+
+// one thread per (n, g): S1, S2 (f32 out, divided by Ng); then one thread per channel: dbeta, dgamma (sum over n)
+__global__ void __launch_bounds__(256) gnb_group_kernel(const double* __restrict__ ab, int n, int c_p, int c,
+                                                        int groups, double ng, const float* __restrict__ gamma,
+                                                        float* __restrict__ s12, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int cpg = c / groups;
+  if (i < n * groups) {
+    const int nn = i / groups, gi = i - (i / groups) * groups;
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < cpg; ++k) {
+      const int cc = gi * cpg + k;
+      s1 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 2];
+      s2 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 2 + 1];
+    }
+    s12[2 * i] = (float)(s1 / ng);
+    s12[2 * i + 1] = (float)(s2 / ng);
+  }
+  if (i < c) {
+    double db = 0.0, dg = 0.0;
+    for (int nn = 0; nn < n; ++nn) {
+      db += ab[((int64_t)nn * c_p + i) * 2];
+      dg += ab[((int64_t)nn * c_p + i) * 2 + 1];
+    }
+    if (dbeta) dbeta[i] = (float)db;
+    if (dgamma) dgamma[i] = (float)dg;
+  }
+}
+
+template <typename TY, typename TD, typename TO>
+__global__ void __launch_bounds__(256) gnb_apply_kernel(const TY* __restrict__ y, const TD* __restrict__ dout,
+                                                        TO* __restrict__ dy, int n, int h, int w, int c_p, int c,
+                                                        int groups, const float* __restrict__ stats,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float slope, int pool,
+                                                        const float* __restrict__ s12) {
+  const int64_t total = (int64_t)n * h * w * c_p;
+  const int cpg = c / groups;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int cc = (int)(e % c_p);
+    const int64_t pix = e / c_p;
+    const int p = (int)(pix % ((int64_t)h * w));
+    const int nn = (int)(pix / ((int64_t)h * w));
+    float v = 0.f;
+    if (cc < c) {
+      const int gi = cc / cpg;
+      const int sidx = nn * groups + gi;
+      const float mean = stats[2 * sidx], rstd = stats[2 * sidx + 1];
+      const float gam = gamma[cc];
+      const int yy = p / w, xx = p - (p / w) * w;
+      float xhat;
+      const float dz = gnb_dz(gld(y, e), gnb_da<TY, TD>(dout, nn, yy, xx, h, w, c_p, cc, pool), mean, rstd, gam,
+                              beta[cc], slope, xhat);
+      v = rstd * (gam * dz - s12[2 * sidx] - xhat * s12[2 * sidx + 1]);
+    }
+    st(dy + e, v);
+  }
+}
+
+// d mean_{hw}(x) / dx: dx[n][p][c] = dpooled[n][c] / hw (padded channels 0)
+template <typename TO>
+__global__ void __launch_bounds__(256) gap_bwd_kernel(const float* __restrict__ dp, TO* __restrict__ dx, int n, int hw,
+                                                      int c_p, int c) {
+  const int64_t total = (int64_t)n * hw * c_p;
+  const float inv = 1.f / (float)hw;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int cc = (int)(e % c_p);
+    const int nn = (int)(e / ((int64_t)hw * c_p));
+    st(dx + e, cc < c ? dp[(int64_t)nn * c + cc] * inv : 0.f);
+  }
+}
+
+static unsigned grid_for(int64_t total) {
+  int64_t g = ceil_div(total, 256);
+  return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace ic2
+
+using namespace ic2;
+
+extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad) {
+  WgradArgs a{};
+  a.ho = h + 2 * pad - kh + 1;
+  a.wo = w + 2 * pad - kw + 1;
+  if (n <= 0 || a.ho <= 0 || a.wo <= 0 || cin_p % 32 || cout_p % 32) return 0;
+  a.P = n * a.ho * a.wo;
+  a.chunks = (int)ceil_div(a.P, WG_KP);
+  a.cout_p = cout_p;
+  a.j_tiles = kh * kw * (int)ceil_div(cin_p, WG_BJ);
+  return (int64_t)wgrad_splits(a) * cout_p * kh * kw * cin_p;
+}
+
+extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
+                              int cout_p, int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream) {
+  IC2_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null pointer");
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_wgrad: bad dtype %d", dtype);
+  IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
+                "conv_wgrad: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
+  IC2_CHECK_ARG(n > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0, "conv_wgrad: bad geometry");
+  WgradArgs a{};
+  a.x = x; a.dy = dy; a.part = workspace;
+  a.n = n; a.h = h; a.w = w; a.cin_p = cin_p; a.cout_p = cout_p; a.kh = kh; a.kw = kw; a.pad = pad;
+  a.ho = h + 2 * pad - kh + 1;
+  a.wo = w + 2 * pad - kw + 1;
+  IC2_CHECK_ARG(a.ho > 0 && a.wo > 0, "conv_wgrad: empty output");
+  IC2_CHECK_ARG((int64_t)n * a.ho * a.wo < (1LL << 30), "conv_wgrad: too many pixels");
+  a.P = n * a.ho * a.wo;
+  a.chunks = (int)ceil_div(a.P, WG_KP);
+  a.j_tiles = kh * kw * (int)ceil_div(cin_p, WG_BJ);
+  const int splits = wgrad_splits(a);
+  const int64_t total = (int64_t)cout_p * kh * kw * cin_p;
+  IC2_CHECK_ARG(ws_floats >= splits * total, "conv_wgrad: workspace too small (%lld < %lld floats)",
+                (long long)ws_floats, (long long)(splits * total));
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((unsigned)(ceil_div(cout_p, WG_BO) * a.j_tiles), (unsigned)splits);
+  if (dtype == IC2_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, s, workspace, dw, total, splits);
+  IC2_CHECK_LAUNCH("conv_wgrad");
+  return IC2_OK;
+}
+
+extern "C" int64_t ic2_gn_lrelu_pool_bwd_floats(int n, int h, int w, int c_p, int groups) {
+  const int64_t nchunks = ceil_div((int64_t)h * w, GNB_CHUNK);
+  // part [n][c_p][nchunks][2] f32 | ab [n][c_p][2] f64 | s12 [n][groups][2] f32
+  return (int64_t)n * c_p * nchunks * 2 + (int64_t)n * c_p * 2 * 2 + (int64_t)n * groups * 2 + 4;
+}
+
+extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout,
+                                     int dtype_dy, int n, int h, int w, int c_p, int c, int groups, const float* stats,
+                                     const float* gamma, const float* beta, float slope, int pool, float* dgamma,
+                                     float* dbeta, float* workspace, int64_t ws_floats, void* stream) {
+  IC2_CHECK_ARG(y && dout && dy && stats && gamma && beta && workspace && n > 0 && h > 0 && w > 0 && c > 0 &&
+                    c <= c_p && groups > 0 && c % groups == 0,
+                "gn_lrelu_pool_bwd: bad arguments");
+  IC2_CHECK_ARG(!pool || (h >= 2 && w >= 2), "gn_lrelu_pool_bwd: pooling needs H, W >= 2");
+  IC2_CHECK_ARG(ws_floats >= ic2_gn_lrelu_pool_bwd_floats(n, h, w, c_p, groups), "gn_lrelu_pool_bwd: workspace too small");
+  IC2_CHECK_ARG((dtype_y == IC2_F32 || dtype_y == IC2_BF16) && (dtype_dout == IC2_F32 || dtype_dout == IC2_BF16) &&
+                    (dtype_dy == IC2_F32 || dtype_dy == IC2_BF16),
+                "gn_lrelu_pool_bwd: bad dtypes");
+  const int nchunks = (int)ceil_div((int64_t)h * w, GNB_CHUNK);
+  float* part = workspace;
+  double* ab = reinterpret_cast<double*>(workspace + (((int64_t)n * c_p * nchunks * 2 + 1) / 2) * 2);
+  float* s12 = reinterpret_cast<float*>(ab + (int64_t)n * c_p * 2);
+  hipStream_t s = as_stream(stream);
+  const double ng = (double)h * w * (c / groups);
+  const int64_t total = (int64_t)n * h * w * c_p;
+#define IC2_GNB(TY, TD)                                                                                          \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((gnb_partial_kernel<TY, TD>), dim3((unsigned)(n * nchunks)), dim3(256), 0, s, (const TY*)y, \
+                       (const TD*)dout, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool, nchunks, part);   \
+    hipLaunchKernelGGL(gnb_chunks_kernel, dim3(grid_for((int64_t)n * c_p)), dim3(256), 0, s, part, n * c_p,        \
+                       nchunks, ab);                                                                             \
+    const int ng_th = n * groups > c ? n * groups : c;                                                           \
+    hipLaunchKernelGGL(gnb_group_kernel, dim3((unsigned)ceil_div(ng_th, 256)), dim3(256), 0, s, ab, n, c_p, c,     \
+                       groups, ng, gamma, s12, dgamma, dbeta);                                                   \
+    if (dtype_dy == IC2_F32)                                                                                     \
+      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, float>), dim3(grid_for(total)), dim3(256), 0, s, (const TY*)y,  \
+                         (const TD*)dout, (float*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,    \
+                         s12);                                                                                   \
+    else                                                                                                         \
+      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, bf16_t>), dim3(grid_for(total)), dim3(256), 0, s, (const TY*)y, \
+                         (const TD*)dout, (bf16_t*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,   \
+                         s12);                                                                                   \
+  } while (0)
+  if (dtype_y == IC2_F32 && dtype_dout == IC2_F32) IC2_GNB(float, float);
+  else if (dtype_y == IC2_F32) IC2_GNB(float, bf16_t);
+  else if (dtype_dout == IC2_F32) IC2_GNB(bf16_t, float);
+  else IC2_GNB(bf16_t, bf16_t);
+#undef IC2_GNB
+  IC2_CHECK_LAUNCH("gn_lrelu_pool_bwd");
+  return IC2_OK;
+}
+
+extern "C" int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_p, int c, void* stream) {
+  IC2_CHECK_ARG(dpooled && dx && n > 0 && hw > 0 && c > 0 && c <= c_p, "gap_bwd: bad arguments");
+  const int64_t total = (int64_t)n * hw * c_p;
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32) hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, s, dpooled,
+                                           (float*)dx, n, hw, c_p, c);
+  else if (dtype == IC2_BF16) hipLaunchKernelGGL(gap_bwd_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, s,
+                                                 dpooled, (bf16_t*)dx, n, hw, c_p, c);
+  else IC2_CHECK_ARG(false, "gap_bwd: bad dtype");
+  IC2_CHECK_LAUNCH("gap_bwd");
+  return IC2_OK;
+}

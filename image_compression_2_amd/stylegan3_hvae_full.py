@@ -24,6 +24,7 @@ import torch.nn.functional as F
 from PIL import Image
 
 from . import _native as nv
+from . import autograd_ops as ao
 
 
 def _version_key(*tensors):
@@ -176,8 +177,11 @@ class HVAE_VGG_Encoder(nn.Module):
         return feats
 
     def forward(self, x):
-        """x [N, C, H, W] f32 in [-1, 1] -> (w_plus, means, logvars), each [N, num_ws, w_dim] f32."""
-        nv.forbid_autograd("HVAE_VGG_Encoder.forward", (x,), (self,))
+        """x [N, C, H, W] f32 in [-1, 1] -> (w_plus, means, logvars), each [N, num_ws, w_dim] f32.
+        With grad mode on and a parameter or x requiring grad (the reference's training loop, :655-707) the same
+        HIP kernels run under autograd (autograd_ops: HIP backward kernels); otherwise the inference path."""
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return self.forward_train(x)
         x = _check_input(x)
         dt = nv.torch_dtype(self.precision)
         stream = nv.stream_of(x)
@@ -190,6 +194,35 @@ class HVAE_VGG_Encoder(nn.Module):
             proj.run_pooled(_gap(feats[key], stream), outs, off, self.num_ws, stream)
             off += proj.num_ws
         return tuple(outs)
+
+
+    def forward_train(self, x):
+        """Autograd path: NHWC activations in the module's precision, HIP forward + backward kernels per op."""
+        x = x.to(torch.float32)
+        nv.require_gpu(x.contiguous())
+        dt = nv.torch_dtype(self.precision)
+        h = ao.ToNHWC.apply(x.contiguous(), dt, nv.pad32(x.shape[1]))
+        h = ao.Conv2dNHWC.apply(h, self.from_rgb.weight, self.from_rgb.bias, self.from_rgb.padding[0],
+                                nv.pad32(self.from_rgb.out_channels))
+        c = self.from_rgb.out_channels
+        feats = {}
+        for i, block in enumerate(self.blocks):
+            if h.shape[1] <= 1 or h.shape[2] <= 1:
+                break
+            h, c = block.forward_train_nhwc(h, dt)
+            if i == self.hierarchy_blocks["fine"]:
+                feats["fine"] = (h, c)
+            elif i == self.hierarchy_blocks["medium"]:
+                feats["medium"] = (h, c)
+        feats["global"] = (h, c)
+        feats.setdefault("fine", (h, c))
+        feats.setdefault("medium", (h, c))
+        outs = []
+        for proj, key in ((self.global_projector, "global"), (self.medium_projector, "medium"),
+                          (self.fine_projector, "fine")):
+            fh, fc = feats[key]
+            outs.append(proj.forward_pooled_train(ao.GlobalAvgPoolNHWC.apply(fh, fc)))
+        return tuple(torch.cat([o[k] for o in outs], dim=1) for k in range(3))
 
 
 class VGGBlock(nn.Module):
@@ -210,6 +243,18 @@ class VGGBlock(nn.Module):
         y = _conv(self.conv2, h, dt, cache, stream)
         pool = y.h > 1 and y.w > 1
         return _group_norm_lrelu(self.norm2, y, pool, dt, stream)
+
+    def forward_train_nhwc(self, h, dt):
+        """Autograd path of run_nhwc: (NHWC activation, valid channels) -> the same after the block."""
+        y = ao.Conv2dNHWC.apply(h, self.conv1.weight, self.conv1.bias, 1, nv.pad32(self.conv1.out_channels))
+        c = self.conv1.out_channels
+        h = ao.GroupNormLReluPoolNHWC.apply(y, self.norm1.weight, self.norm1.bias, self.norm1.num_groups,
+                                            self.norm1.eps, 0.2, False, c, dt)
+        y = ao.Conv2dNHWC.apply(h, self.conv2.weight, self.conv2.bias, 1, nv.pad32(self.conv2.out_channels))
+        pool = y.shape[1] > 1 and y.shape[2] > 1
+        h = ao.GroupNormLReluPoolNHWC.apply(y, self.norm2.weight, self.norm2.bias, self.norm2.num_groups,
+                                            self.norm2.eps, 0.2, pool, c, dt)
+        return h, c
 
     def forward(self, x):
         nv.forbid_autograd("VGGBlock.forward", (x,), (self,))
@@ -244,6 +289,19 @@ class HierarchyProjector(nn.Module):
         w_out, m_out, lv_out = outs
         nv.call("ic2_reparameterize", nv.ptr(p), nv.ptr(eps), n, self.num_ws, self.w_dim, ws_total, off, nv.ptr(w_out),
                 nv.ptr(m_out), nv.ptr(lv_out), stream)
+
+    def forward_pooled_train(self, pooled):
+        """Autograd path of run_pooled (torch ops on [N, <= 512] rows): -> (w, mean, logvar)."""
+        n, in_features = pooled.shape
+        if in_features != self.in_channels:
+            # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
+            self.fc1 = nn.Linear(in_features, 256).to(pooled.device)
+        h = F.leaky_relu(F.linear(pooled, self.fc1.weight, self.fc1.bias), self.act.negative_slope)
+        p = F.linear(h, self.fc2.weight, self.fc2.bias).view(n, self.num_ws, self.w_dim * 2)
+        mean, logvar = torch.chunk(p, 2, dim=2)
+        std = torch.exp(0.5 * logvar)
+        eps = torch.randn([n, self.num_ws, self.w_dim], dtype=torch.float32, device=pooled.device)
+        return mean + eps * std, mean, logvar
 
     def forward(self, x):
         nv.forbid_autograd("HierarchyProjector.forward", (x,), (self,))

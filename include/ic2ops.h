@@ -210,6 +210,31 @@ int ic2_rc_encode(const int32_t* codes, int64_t n_streams, int num_ws, int w_dim
 int ic2_rc_decode(const uint8_t* in, const int64_t* stream_bytes, int64_t n_streams, int num_ws, int w_dim,
                   int n_symbols, int32_t* codes_out, int n_threads);
 
+/* ---- training path (BASELINE C5; the reference's train_hvae_encoder backward, stylegan3_hvae_full.py:693-696:
+ * torch autograd through HVAE_VGG_Encoder).  The conv input gradient is ic2_conv_igemm on flipped / transposed
+ * weights; these are the remaining encoder backward ops. ---- */
+
+/* nn.Conv2d weight gradient (VGGBlock.conv1/conv2, from_rgb: :62, :175-176): dw [cout_p][kh][kw][cin_p] f32 =
+ * sum over output pixels of dy[p][o] * x[p shifted by the tap][i]; x NHWC [n][h][w][cin_p], dy NHWC
+ * [n][ho][wo][cout_p] (dtype f32 / bf16, channel strides multiples of 32), stride 1, zero padding `pad`.
+ * Workspace: ic2_conv_wgrad_ws_floats() floats (per-slice partial sums, reduced in slice order). */
+int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad);
+int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p, int cout_p,
+                   int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream);
+
+/* Backward of ic2_gn_lrelu_pool (VGGBlock :183-191: GroupNorm -> leaky_relu(0.2) -> AvgPool2d(2) when `pool`):
+ * y = the GroupNorm input (NHWC [n][h][w][c_p]), stats = ic2_group_norm_stats' output, dout = gradient of the
+ * block output (pooled resolution when `pool`) -> dy (NHWC, same shape as y), dgamma, dbeta [c] (nullable).
+ * dtypes f32 / bf16 each.  Workspace: ic2_gn_lrelu_pool_bwd_floats() floats.  Deterministic. */
+int64_t ic2_gn_lrelu_pool_bwd_floats(int n, int h, int w, int c_p, int groups);
+int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout, int dtype_dy, int n,
+                          int h, int w, int c_p, int c, int groups, const float* stats, const float* gamma,
+                          const float* beta, float slope, int pool, float* dgamma, float* dbeta, float* workspace,
+                          int64_t ws_floats, void* stream);
+
+/* Backward of ic2_global_avg_pool (AdaptiveAvgPool2d(1), :218): dx [n][hw][c_p] = dpooled [n][c] / hw. */
+int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_p, int c, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -313,8 +313,8 @@ def test_forwards_refuse_autograd_on_gpu(cuda, gen256):
     with torch.enable_grad():
         enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32).to(cuda)
         x = torch.rand(1, 3, 32, 32, device=cuda)
-        with pytest.raises(nv.AutogradUnsupported):
-            enc(x)
+        w, m, lv = enc(x)  # the encoder has a HIP autograd path (test_gpu_training.py)
+        assert m.grad_fn is not None
         ws = torch.zeros(1, 16, 512, device=cuda, requires_grad=True)
         with pytest.raises(nv.AutogradUnsupported):
             gen256.synthesis(ws)

@@ -56,8 +56,8 @@ def test_forwards_refuse_autograd():
     and a parameter or input requiring grad, every HIP forward raises before touching the device."""
     enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32, w_dim=32)
     x = torch.zeros(1, 3, 32, 32)
-    with pytest.raises(nv.AutogradUnsupported):
-        enc(x)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        enc(x)   # the encoder trains through its HIP autograd path (autograd_ops); no CPU fallback either way
     with pytest.raises(nv.AutogradUnsupported):
         enc.blocks[0](torch.zeros(1, 32, 8, 8))
     G = ic2.Generator(img_resolution=256)
