@@ -13,6 +13,16 @@ HIP kernel as well (csrc/backward.hip, or the forward implicit GEMM on transform
 Activations are NHWC with padded channel strides, in the module's precision (f32 parity mode / bf16);
 gradients flow in the same layout and dtype; weight gradients are f32.  The projector MLPs are [N, <=512]
 matrices and run as torch ops on the device.
+
+The encoder's loss reaches it through the FROZEN StyleGAN3 synthesis network (:671-674, the generator's
+parameters are frozen at :259-261), so the synthesis layers need gradients w.r.t. their input activations and
+their styles only:
+
+    modulated conv (SG3 modulated_conv2d)  fwd ic2_conv_igemm (normalised W)   bwd dx: ic2_conv_igemm on the
+                                                                                 flipped, transposed W
+    filtered lrelu (SG3 filtered_lrelu)    fwd ic2_flrelu_nhwc                bwd recompute up(z); adjoint
+                                                                                 FIRs via ic2_upfirdn2d
+    styles / (de)modulation / Fourier input    torch ops on [N, <= 512] rows and the 36x36 input grid
 """
 from __future__ import annotations
 
@@ -168,3 +178,60 @@ class ToNHWC(torch.autograd.Function):
         nv.call("ic2_nhwc_to_nchw", nv.ptr(dy), nv.dtype_code(dy.dtype), nv.ptr(dx), n, c, h, w, dy.shape[-1],
                 nv.stream_of(dy))
         return dx, None, None
+
+
+class FrozenConvNHWC(torch.autograd.Function):
+    """Conv with constant, pre-packed weights (the modulated conv of a frozen SG3 layer, whose per-sample
+    modulation is applied outside as xscale / oscale): output f32, gradient w.r.t. the input only.
+    wp [cout_p][k][k][cin_p] and wt = the flipped, channel-transposed pack [cin_p][k][k][cout_p]."""
+
+    @staticmethod
+    def forward(ctx, x, wp, wt, k, pad, cout, cin):
+        y = conv_nhwc(x, wp, None, cout, k, pad, dt_out=torch.float32)
+        ctx.wt, ctx.meta = wt, (k, pad, cin, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        k, pad, cin, dt = ctx.meta
+        dx = conv_nhwc(dy.to(dt).contiguous(), ctx.wt, None, cin, k, k - 1 - pad)
+        return dx, None, None, None, None, None, None
+
+
+def _flr_chunk(n, c, hu, wu):
+    """Samples per backward chunk: keep the recomputed upsampled planes (f32, ~3 live copies) near 2 GiB."""
+    per = max(1, c * hu * wu * 4 * 3)
+    return max(1, min(n, (2 << 30) // per))
+
+
+class FilteredLReluNHWC(torch.autograd.Function):
+    """SG3 filtered_lrelu on NHWC activations with the layer's filters, padding, gain sqrt(2), slope 0.2 and
+    clamp (SynthesisLayer.forward).  Forward: the fused HIP kernel.  Backward: per chunk of samples, NCHW f32
+    planes of the valid channels through sg3_ops.filtered_lrelu_backward (HIP upfirdn2d kernels)."""
+
+    @staticmethod
+    def forward(ctx, y, layer, dt_out):
+        out = layer.flrelu_nhwc(y, dt_out)
+        ctx.save_for_backward(y)
+        ctx.layer = layer
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import sg3_ops
+        (y,) = ctx.saved_tensors
+        L = ctx.layer
+        n, h, w, c_p = y.shape
+        c = L.out_channels
+        dy = torch.zeros_like(y)
+        hu = h * L.up_factor + L.padding[2] + L.padding[3] - (L.up_taps - 1)
+        wu = w * L.up_factor + L.padding[0] + L.padding[1] - (L.up_taps - 1)
+        step = _flr_chunk(n, c, hu, wu)
+        clamp = float(L.conv_clamp) if L.conv_clamp is not None else None
+        for i in range(0, n, step):
+            z = y[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
+            g = dout[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
+            dz = sg3_ops.filtered_lrelu_backward(z, g, L.up_filter, L.down_filter, L.up_factor, L.down_factor,
+                                                 L.padding, L.act_gain, 0.2, clamp)
+            dy[i:i + step, :, :, :c] = dz.permute(0, 2, 3, 1).to(y.dtype)
+        return dy, None, None

@@ -1,6 +1,10 @@
 """Batch-sharded data parallelism: one process per GPU, contiguous batch slices,
 no data-path collective; one all_reduce(SUM) of a small fp64 metric vector per batch over RCCL
-(backend "nccl" on ROCm) -- gloo on CPU for tests.  The reference has no distributed code."""
+(backend "nccl" on ROCm) -- gloo on CPU for tests.  The reference has no distributed code.
+
+Training (BASELINE C5, data parallel): each rank backpropagates its own batch slice and the encoder's
+gradients are averaged with ``allreduce_gradients`` -- bucketed flat all_reduce(SUM) / world, the only
+collective of the step (the generator is frozen and has no gradients)."""
 from __future__ import annotations
 
 import os
@@ -100,3 +104,34 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+def allreduce_gradients(params, world=None, bucket_bytes=64 << 20):
+    """Average the .grad of ``params`` over ranks in place: grads are packed into flat f32 buckets of about
+    ``bucket_bytes`` (one all_reduce per bucket: the encoder's ~26 M gradients are two RCCL calls, large
+    enough to run at xGMI ring bandwidth) and copied back divided by the world size.  Parameters without a
+    gradient are skipped; every rank runs the same module graph, so the bucket layout agrees across ranks."""
+    if world is None:
+        world = dist.get_world_size() if dist.is_initialized() else 1
+    grads = [p.grad for p in params if p.grad is not None]
+    if world <= 1 or not grads:
+        return 0
+    buckets, cur, size = [], [], 0
+    for g in grads:
+        cur.append(g)
+        size += g.numel() * 4
+        if size >= bucket_bytes:
+            buckets.append(cur)
+            cur, size = [], 0
+    if cur:
+        buckets.append(cur)
+    for b in buckets:
+        flat = torch.cat([g.reshape(-1).to(torch.float32) for g in b])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.div_(world)
+        off = 0
+        for g in b:
+            k = g.numel()
+            g.copy_(flat[off:off + k].view_as(g))
+            off += k
+    return len(buckets)

@@ -15,6 +15,10 @@ seeded parameter construction order, and a forward that runs entirely in libic2o
 ``precision='bf16'`` stores activations and weights in bf16 (fp32 accumulate; the conv output that feeds
 the filtered lrelu is f16, whose FIR runs on MFMA with f16 operands and fp32 accumulation);
 ``precision='fp32'`` (default) is the parity mode (exact-fp32 MFMA).
+
+With grad mode on and ``ws`` requiring grad (the reference's encoder training backpropagates through the
+frozen generator, :669-696) ``SynthesisNetwork.forward`` takes the autograd path ``forward_train``: the same
+conv / filtered-lrelu kernels with HIP backward passes (autograd_ops), gradients w.r.t. ws only.
 """
 from __future__ import annotations
 
@@ -24,9 +28,28 @@ import math
 import numpy as np
 import scipy.signal
 import torch
+import torch.nn.functional as F
 
 from . import _native as nv
+from . import autograd_ops as ao
 from . import sg3_ops
+
+
+def _train_mode(module, *tensors):
+    """Autograd path wanted: grad mode on and an input requires grad.  Generator weights are frozen on that
+    path (the reference freezes G, stylegan3_hvae_full.py:259-261); weight gradients are refused."""
+    if not torch.is_grad_enabled():
+        return False
+    params = any(p.requires_grad for p in module.parameters())
+    if not any(t is not None and t.requires_grad for t in tensors):
+        if params:
+            nv.forbid_autograd(type(module).__name__ + ".forward", (), (module,))
+        return False
+    if params:
+        raise nv.AutogradUnsupported(
+            f"{type(module).__name__}.forward: gradients w.r.t. the generator's weights are not implemented "
+            "(the reference trains its encoder through a frozen G): call .requires_grad_(False) on the generator")
+    return True
 
 
 def _version_key(*tensors):
@@ -157,8 +180,34 @@ class SynthesisInput(torch.nn.Module):
                       feats.device)
         return out
 
+    def forward_train_nhwc(self, w):
+        """Autograd path: w [n, w_dim] -> NHWC [n, S, S, C] f32 features, as torch ops (SG3
+        SynthesisInput.forward: affine -> rotation/translation of the Fourier frequencies -> sin features with
+        the bandwidth taper -> 1x1 mix by weight / sqrt(C); the grid is 36 x 36 and the rows are <= 512 wide)."""
+        A = self.affine
+        t = F.linear(w, A.weight * float(A.weight_gain), A.bias * float(A.bias_gain))
+        t = t / t[:, :2].norm(dim=1, keepdim=True)
+        zero, one = torch.zeros_like(t[:, 0]), torch.ones_like(t[:, 0])
+        m_r = torch.stack([torch.stack([t[:, 0], -t[:, 1], zero], 1), torch.stack([t[:, 1], t[:, 0], zero], 1),
+                           torch.stack([zero, zero, one], 1)], 1)
+        m_t = torch.stack([torch.stack([one, zero, -t[:, 2]], 1), torch.stack([zero, one, -t[:, 3]], 1),
+                           torch.stack([zero, zero, one], 1)], 1)
+        transforms = m_r @ m_t @ self.transform.float().unsqueeze(0)
+        freqs = self.freqs.float().unsqueeze(0)
+        phases = self.phases.float().unsqueeze(0) + (freqs @ transforms[:, :2, 2:]).squeeze(2)
+        freqs = freqs @ transforms[:, :2, :2]
+        amplitudes = (1 - (freqs.norm(dim=2) - self.bandwidth) / (self.sampling_rate / 2 - self.bandwidth)).clamp(0, 1)
+        S = int(self.size[0])
+        theta = torch.tensor([[0.5 * S / self.sampling_rate, 0, 0], [0, 0.5 * S / self.sampling_rate, 0]],
+                             dtype=torch.float32, device=w.device)
+        grids = F.affine_grid(theta.unsqueeze(0), [1, 1, S, S], align_corners=False)     # [1, S, S, 2]
+        x = (grids.unsqueeze(3) @ freqs.permute(0, 2, 1).unsqueeze(1).unsqueeze(2)).squeeze(3)
+        x = torch.sin((x + phases[:, None, None, :]) * (np.pi * 2)) * amplitudes[:, None, None, :]
+        return x @ (self.weight.float() / np.sqrt(self.channels)).t()
+
     def forward(self, w):
-        nv.forbid_autograd("SynthesisInput.forward", (w,), (self,))
+        if _train_mode(self, w):
+            return self.forward_train_nhwc(w.to(torch.float32)).permute(0, 3, 1, 2).contiguous()
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(w)
         n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad_synth(self.channels)
@@ -307,25 +356,83 @@ class SynthesisLayer(torch.nn.Module):
         nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
                       self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
                       0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.device)
+        return self.flrelu_nhwc(y, dt, post_scale)
+
+    def flrelu_nhwc(self, y, dt_out, post_scale=None):
+        """The layer's filtered lrelu on the conv output y NHWC [n, conv, conv, cout_p] (f32, or f16 for the
+        MFMA kernel) -> NHWC [n, out, out, cout_p] dt_out, times post_scale [n][cout_p] when given."""
+        n, conv = y.shape[0], y.shape[1]
         s_out = int(self.out_size[0])
-        out = torch.empty([n, s_out, s_out, self.cout_p], dtype=dt, device=x.device)
+        out = torch.empty([n, s_out, s_out, self.cout_p], dtype=dt_out, device=y.device)
         fu = self._fu
         fd = self._fd
         px0, px1, py0, py1 = self.padding
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
-        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(ydt), nv.dtype_code(dt), n, self.cout_p, conv,
-                conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
+        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(y.dtype), nv.dtype_code(dt_out), n,
+                self.cout_p, conv, conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
                 1 if fu is None else fu.shape[0], None if fd is None else fd.ctypes.data_as(ctypes.c_void_p),
                 1 if fd is None else fd.shape[0], None, self.up_factor, self.down_factor, px0, px1, py0, py1,
-                float(self.act_gain), 0.2, clamp, 0, nv.ptr(post_scale), stream)
+                float(self.act_gain), 0.2, clamp, 0, nv.ptr(post_scale), nv.stream_of(y))
         return out
+
+    # ---- autograd path: gradients w.r.t. the input activation and w (weights frozen) ----------------------
+    def packed_adjoint(self, dt):
+        """The dgrad weights: normalised W flipped in space, transposed in channels, packed
+        [cin_p][k][k][cout_p] (dt) -- the forward igemm on these is the modulated conv's adjoint."""
+        key = (dt, _version_key(self.weight))
+        hit = self._cache.get(("adj", dt))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w = self.weight.detach().to(torch.float32)
+        if not self.is_torgb:
+            w = w * w.square().mean(dim=[1, 2, 3], keepdim=True).rsqrt()
+        wt = ao.pack_conv_weight(w.transpose(0, 1).flip(2, 3), self.cout_p, self.cin_p, dt)
+        self._cache[("adj", dt)] = (key, wt)
+        return wt
+
+    def modulation_train(self, w):
+        """Differentiable (xscale [n][cin_p], oscale [n][cout_p]) f32 from w [n, w_dim]: the same math as
+        ic2_modconv_prep (styles = affine(w); demodulated layers: s * rsqrt(mean s^2) over the whole batch,
+        oscale = input_gain * rsqrt(sum_i s_i^2 wsq[o, i] + 1e-8); ToRGB: s / sqrt(cin k^2), oscale =
+        input_gain), as torch ops on [n, <= 512] rows."""
+        A = self.affine
+        styles = F.linear(w, A.weight * float(A.weight_gain), A.bias * float(A.bias_gain))
+        ig = self.input_gain()
+        if self.is_torgb:
+            s = styles * float(1 / np.sqrt(self.in_channels * (self.conv_kernel ** 2)))
+            d = torch.full([w.shape[0], self.out_channels], ig, dtype=torch.float32, device=w.device)
+        else:
+            s = styles * styles.square().mean().rsqrt()
+            _, wsq, _ = self.packed(torch.float32)
+            d = (s.square() @ wsq.t() + 1e-8).rsqrt() * ig
+        return F.pad(s, (0, self.cin_p - self.in_channels)), F.pad(d, (0, self.cout_p - self.out_channels))
+
+    def forward_train_nhwc(self, x, w, dt, final_scale=None):
+        """Autograd step: x NHWC [n, in, in, cin_p] (dt, NOT yet scaled by xscale), w [n, w_dim] f32 ->
+        NHWC [n, out, out, cout_p] dt, or for ToRGB the NCHW f32 image * final_scale."""
+        xs, os_ = self.modulation_train(w)
+        a = x * xs[:, None, None, :].to(x.dtype)
+        k = self.conv_kernel
+        wp, _, bp = self.packed(dt)
+        c = ao.FrozenConvNHWC.apply(a, wp, self.packed_adjoint(dt), k, k - 1, self.out_channels, self.in_channels)
+        y = c * os_[:, None, None, :] + bp
+        if self.is_torgb:
+            if self.conv_clamp is not None:
+                y = y.clamp(-float(self.conv_clamp), float(self.conv_clamp))
+            img = y[..., : self.out_channels].permute(0, 3, 1, 2)
+            return img if final_scale is None else img * float(final_scale)
+        if dt == torch.bfloat16:
+            # the MFMA filtered lrelu takes f16 operands; the inference epilogue saturates at the f16 range
+            y = y.clamp(-65504.0, 65504.0).to(torch.float16)
+        return ao.FilteredLReluNHWC.apply(y, self, dt)
 
     def forward(self, x, w, noise_mode="random", force_fp32=False, update_emas=False):
         """Layer-level API (NCHW f32 in/out), as SG3's SynthesisLayer.forward."""
         assert noise_mode in ("random", "const", "none")
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
-        nv.forbid_autograd("SynthesisLayer.forward", (x, w), (self,))
+        if _train_mode(self, x, w):
+            return self.forward_train(x, w)
         x = x.to(torch.float32).contiguous()
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(x, w)
@@ -345,6 +452,17 @@ class SynthesisLayer(torch.nn.Module):
         nv.call("ic2_nhwc_to_nchw", nv.ptr(out), nv.F32, nv.ptr(y), n, self.out_channels, s_out, s_out, self.cout_p,
                 nv.stream_of(x))
         return y
+
+    def forward_train(self, x, w):
+        """Layer-level autograd path (NCHW f32 in/out), fp32."""
+        x = x.to(torch.float32)
+        w = w.to(torch.float32)
+        nv.require_gpu(x.contiguous(), w.contiguous())
+        xn = F.pad(x.permute(0, 2, 3, 1), (0, self.cin_p - self.in_channels)).contiguous()
+        out = self.forward_train_nhwc(xn, w, torch.float32)
+        if self.is_torgb:
+            return out
+        return out[..., : self.out_channels].permute(0, 3, 1, 2).contiguous()
 
     @staticmethod
     def design_lowpass_filter(numtaps, cutoff, width, fs, radial=False):
@@ -426,10 +544,11 @@ class SynthesisNetwork(torch.nn.Module):
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
         assert ws.ndim == 3 and ws.shape[1] == self.num_ws and ws.shape[2] == self.w_dim, ws.shape
-        nv.forbid_autograd("SynthesisNetwork.forward", (ws,), (self,))
+        dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
+        if _train_mode(self, ws):
+            return self.forward_train(ws, dt)
         ws = ws.to(torch.float32).contiguous()
         nv.require_gpu(ws)
-        dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
         n = ws.shape[0]
         ldx = self.num_ws * self.w_dim
         layers = self.layers()
@@ -440,6 +559,20 @@ class SynthesisNetwork(torch.nn.Module):
         for i, L in enumerate(layers):
             post = sc[i + 1][0] if i + 1 < len(layers) else None
             x = L.run_nhwc(x, n, dt, sc[i][1], post, final_scale=self.output_scale if L.is_torgb else None)
+        return x
+
+    def forward_train(self, ws, dt):
+        """Autograd path w.r.t. ws (the reference's encoder training, stylegan3_hvae_full.py:669-696): input
+        features and per-layer (de)modulation as torch ops on small tensors, the convs and filtered lrelus as
+        HIP kernels with HIP backward passes (autograd_ops).  The generator's weights stay frozen."""
+        ws = ws.to(torch.float32)
+        nv.require_gpu(ws.contiguous())
+        C = self.input.channels
+        x = self.input.forward_train_nhwc(ws[:, 0])
+        layers = self.layers()
+        x = F.pad(x, (0, layers[0].cin_p - C)).to(dt)
+        for i, L in enumerate(layers):
+            x = L.forward_train_nhwc(x, ws[:, i + 1], dt, final_scale=self.output_scale if L.is_torgb else None)
         return x
 
     def extra_repr(self):

@@ -327,8 +327,7 @@ def quantize_uniform(w, bits=8, return_indices=False):
     return (q, idx) if return_indices else q
 
 
-def resize_bilinear(img, size):
-    """F.interpolate(img, size, mode='bilinear', align_corners=False) (ref ``:277-279``)."""
+def _resize_fwd(img, size):
     img = img.to(torch.float32).contiguous()
     nv.require_gpu(img)
     n, c, h, w = img.shape
@@ -336,6 +335,28 @@ def resize_bilinear(img, size):
     out = torch.empty([n, c, oh, ow], dtype=torch.float32, device=img.device)
     nv.call("ic2_resize_bilinear", nv.ptr(img), nv.ptr(out), n * c, h, w, oh, ow, nv.stream_of(img))
     return out
+
+
+class _ResizeBilinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, size):
+        ctx.in_size = tuple(img.shape)
+        return _resize_fwd(img, size)
+
+    @staticmethod
+    def backward(ctx, dy):
+        # the adjoint of the 4-tap bilinear gather is a scatter-add: torch's own upsample backward on the device
+        dx = torch.ops.aten.upsample_bilinear2d_backward(dy.contiguous(), list(dy.shape[2:]), list(ctx.in_size),
+                                                         False, None, None)
+        return dx, None
+
+
+def resize_bilinear(img, size):
+    """F.interpolate(img, size, mode='bilinear', align_corners=False) (ref ``:277-279``); differentiable (the
+    compressor's training forward resizes the synthesized image back to the training resolution)."""
+    if torch.is_grad_enabled() and img.requires_grad:
+        return _ResizeBilinear.apply(img, tuple(size))
+    return _resize_fwd(img, size)
 
 
 class StyleGAN3Compressor(nn.Module):

@@ -1,0 +1,71 @@
+"""Encoder training step: the body of the reference's ``train_hvae_encoder`` loop (BASELINE config C5,
+/root/reference/stylegan3_hvae_full.py:383-707, step at :655-707), on the HIP autograd path.
+
+Per batch, as the reference:
+    optimizer.zero_grad()                                       :664
+    reconstructed, w_plus = compressor(images)                  :669  encoder (HIP fwd/bwd) -> frozen G.synthesis
+    rec_loss = F.mse_loss(images, reconstructed)                :672
+    perceptual = percep(images, reconstructed).mean()           :675  (LPIPS; see below)
+    _, means, logvars = encoder(images)                         :678  a second encoder pass, as the reference
+    kl = 0.5 * mean_n sum_{ws, c} ((means - w_avg)^2 + exp(lv) - lv - 1)      :679-683
+    loss = rec_weight * rec + perceptual_weight * perceptual + kl_weight * kl  :686-688
+    loss.backward(); optimizer.step()                           :699-701  (Adam(lr, (0.9, 0.999)), :484)
+
+Deviations, all explicit:
+  * LPIPS(net='vgg') needs pretrained VGG weights that cannot be fetched here (no network): ``percep`` is a
+    caller-supplied callable; with ``percep=None`` a non-zero ``perceptual_weight`` raises.
+  * Without fp16 the reference runs its forward under ``torch.no_grad()`` (:668) and its loss.backward()
+    then fails; this step always builds the graph (the reference's fp16 branch: autocast + GradScaler; here
+    ``precision='bf16'`` on the modules, which needs no loss scaling).
+  * Multi-GPU: data parallel, one process per GPU, gradients averaged by distributed.allreduce_gradients.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import distributed as icd
+
+
+def kl_divergence(means, logvars, w_avg):
+    """KL(q(w | x) || N(w_avg, I)) summed over [num_ws, w_dim] and averaged over the batch (ref :679-683)."""
+    return 0.5 * torch.mean(torch.sum(torch.pow(means - w_avg, 2) + torch.exp(logvars) - logvars - 1, dim=[1, 2]))
+
+
+def make_optimizer(encoder, lr=1e-4):
+    """The reference's optimizer (:484)."""
+    return torch.optim.Adam(encoder.parameters(), lr=lr, betas=(0.9, 0.999))
+
+
+def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_weight=0.8, kl_weight=0.01,
+               percep=None, second_encoder_pass=True, sync_gradients=None):
+    """One optimisation step; returns the four losses as 0-d device tensors (no host sync).
+
+    ``w_avg``: G.mapping.w_avg shaped [1, 1, w_dim] (ref :626).  ``second_encoder_pass=False`` reuses the
+    first pass's means / logvars for the KL term (identical values unless the projector's fc1 quirk redraws
+    fc1, ref :225-230) and skips one encoder forward.  ``sync_gradients``: world size for the data-parallel
+    gradient average (default: the initialised process group's)."""
+    if percep is None and perceptual_weight != 0:
+        raise ValueError("perceptual_weight != 0 needs a perceptual loss callable (the reference's LPIPS(net='vgg') "
+                         "weights are not available offline): pass percep=... or perceptual_weight=0")
+    encoder = compressor.encoder
+    optimizer.zero_grad()
+    with torch.enable_grad():
+        if second_encoder_pass:
+            reconstructed, _ = compressor(images)
+            _, means, logvars = encoder(images)
+        else:
+            w_plus, means, logvars = encoder(images)
+            reconstructed = compressor.generator.synthesis(w_plus, noise_mode="const")
+            if compressor.training_resolution is not None and reconstructed.shape[2] != images.shape[2]:
+                from .stylegan3_hvae_full import resize_bilinear
+                reconstructed = resize_bilinear(reconstructed, (images.shape[2], images.shape[3]))
+        rec_loss = F.mse_loss(images, reconstructed)
+        perceptual = percep(images, reconstructed).mean() if percep is not None else rec_loss.new_zeros(())
+        kl = kl_divergence(means, logvars, w_avg)
+        loss = rec_weight * rec_loss + perceptual_weight * perceptual + kl_weight * kl
+        loss.backward()
+    icd.allreduce_gradients(list(encoder.parameters()), sync_gradients)
+    optimizer.step()
+    return {"rec_loss": rec_loss.detach(), "kl_loss": kl.detach(), "perceptual_loss": perceptual.detach(),
+            "total_loss": loss.detach()}

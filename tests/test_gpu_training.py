@@ -145,3 +145,223 @@ def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
     tol = 1e-4 if dtype == torch.float32 else 3e-2
     assert _rel(yd.grad.float().cpu()[..., :c].permute(0, 3, 1, 2), yr.grad) < tol
     assert _rel(gd.grad, gr.grad) < tol and _rel(bd.grad, br.grad) < tol
+
+
+# ================================================================ synthesis backward (the frozen generator)
+from image_compression_2_amd import sg3_ops  # noqa: E402
+from image_compression_2_amd import training as ict  # noqa: E402
+from oracle import sg3  # noqa: E402
+
+
+def _sd64(module):
+    return {k: v.detach().double().cpu() for k, v in module.state_dict().items()}
+
+
+@pytest.fixture(scope="module")
+def gen256_frozen(cuda):
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=256).to(cuda).eval().requires_grad_(False)
+    with torch.no_grad():  # non-unit input gains, as in a trained generator
+        for i, L in enumerate(G.synthesis.layers()):
+            L.magnitude_ema.fill_(0.6 + 0.05 * i)
+    return G
+
+
+@pytest.mark.parametrize("h,w,taps,up,down,pad,flip", [(12, 14, 12, 2, 1, [7, 6, 7, 6], False),
+                                                       (30, 30, 12, 1, 2, 0, False),
+                                                       (9, 11, 24, 4, 1, [13, 11, 14, 10], True),
+                                                       (10, 10, 5, 2, 2, [1, 3, 2, 0], False)])
+def test_sg3_upfirdn2d_gradient(cuda, h, w, taps, up, down, pad, flip):
+    g = torch.Generator().manual_seed(taps + h)
+    x = torch.randn(2, 5, h, w, generator=g)
+    f = torch.rand(taps, generator=g) + 0.1
+    xd = x.to(cuda).requires_grad_(True)
+    y = sg3_ops.upfirdn2d(xd, f.to(cuda), up=up, down=down, padding=pad, flip_filter=flip, gain=up * up)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(cuda))
+    xr = x.double().requires_grad_(True)
+    sg3.upfirdn2d(xr, f.double(), up=up, down=down, padding=pad, flip_filter=flip, gain=up * up).backward(dy.double())
+    assert _rel(xd.grad, xr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("act,clamp", [("lrelu", 1.0), ("linear", 0.5), ("lrelu", None)])
+def test_sg3_bias_act_gradient(cuda, act, clamp):
+    g = torch.Generator().manual_seed(11)
+    x, b = torch.randn(3, 7, 9, 9, generator=g), torch.randn(7, generator=g) * 0.3
+    xd, bd = x.to(cuda).requires_grad_(True), b.to(cuda).requires_grad_(True)
+    y = sg3_ops.bias_act(xd, bd, act=act, clamp=clamp)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(cuda))
+    xr, br = x.double().requires_grad_(True), b.double().requires_grad_(True)
+    sg3.bias_act(xr, br, act=act, clamp=clamp).backward(dy.double())
+    assert _rel(xd.grad, xr.grad) < 1e-6 and _rel(bd.grad, br.grad) < 1e-6
+
+
+@pytest.mark.parametrize("li", [2, 5, 12])
+def test_sg3_filtered_lrelu_gradient(cuda, li):
+    """SG3-T-256 layer geometries (up 2/4, down 2, 12/24 taps, the layer's crop padding), bias, clamp 256 hit.
+    (An element of the upsampled plane within f32 rounding of the clamp edge takes the other side of the mask
+    than in fp64 -- one such tie moves the relative error to ~5e-4 on a 556^2 plane -- hence 40^2 planes.)"""
+    _, layers = sg3.layer_table(256)
+    L = layers[li]
+    g = torch.Generator().manual_seed(li)
+    s = 40   # the geometry (up, down, taps, padding) is the layer's; a small plane keeps clamp-edge ties improbable
+    x = torch.randn(2, 6, s, s, generator=g) * 30 + torch.linspace(-300, 300, 6).view(1, 6, 1, 1)
+    b = torch.randn(6, generator=g)
+    fu, fd = L["up_filter"], L["down_filter"]
+    xd, bd = x.to(cuda).requires_grad_(True), b.to(cuda).requires_grad_(True)
+    y = sg3_ops.filtered_lrelu(xd, fu.to(cuda), fd.to(cuda), bd, up=L["up"], down=L["down"], padding=L["padding"],
+                               clamp=256)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(cuda))
+    xr, br = x.double().requires_grad_(True), b.double().requires_grad_(True)
+    yr = sg3.filtered_lrelu(xr, fu.double(), fd.double(), br, up=L["up"], down=L["down"], padding=L["padding"],
+                            clamp=256)
+    u = sg3.upfirdn2d(xr.detach() + br.detach().view(1, -1, 1, 1), fu.double(), up=L["up"], padding=L["padding"],
+                      gain=L["up"] ** 2)
+    assert (u.abs() * np.sqrt(2) >= 256).any()   # the clamp mask takes part
+    yr.backward(dy.double())
+    assert _rel(xd.grad, xr.grad) < 1e-5 and _rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("li", [0, 3, 8, 13, 14])
+def test_synthesis_layer_gradients_fp32(cuda, gen256_frozen, li):
+    """SynthesisLayer(x, w) with grad: d/dx and d/dw against autograd through the oracle layer in fp64.
+    Tolerance 1e-3: the lrelu derivative jumps at 0, and upsampled elements within f32 rounding of 0 take the
+    other slope than in fp64 -- measured 2e-5 .. 2e-4 relative, growing with the plane (148^2 x 512 x up 2)."""
+    sd = _sd64(gen256_frozen)
+    _, layers = sg3.layer_table(256)
+    L = layers[li]
+    g = torch.Generator().manual_seed(20 + li)
+    x = torch.randn(2, L["in_channels"], L["in_size"], L["in_size"], generator=g)
+    w = torch.randn(2, 512, generator=g)
+    xd, wd = x.to(cuda).requires_grad_(True), w.to(cuda).requires_grad_(True)
+    y = getattr(gen256_frozen.synthesis, L["name"])(xd, wd)
+    r = torch.randn(y.shape, generator=g)
+    (y * r.to(cuda)).sum().backward()
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    yr = sg3.synthesis_layer(sd, L, xr, wr, dtype=torch.float64)
+    assert (y.detach().cpu().double() - yr.detach()).abs().max().item() < 1e-4 * (1 + yr.abs().max().item())
+    (yr * r.double()).sum().backward()
+    ex, ew = _rel(xd.grad, xr.grad), _rel(wd.grad, wr.grad)
+    print(f"[{L['name']}] rel grad error x {ex:.2e} w {ew:.2e}")
+    assert ex < 1e-3 and ew < 1e-3
+
+
+def test_synthesis_input_gradient(cuda, gen256_frozen):
+    sd = _sd64(gen256_frozen)
+    inp, _ = sg3.layer_table(256)
+    w = torch.randn(3, 512, generator=torch.Generator().manual_seed(4))
+    wd = w.to(cuda).requires_grad_(True)
+    y = gen256_frozen.synthesis.input(wd)
+    r = torch.randn(y.shape, generator=torch.Generator().manual_seed(5))
+    (y * r.to(cuda)).sum().backward()
+    wr = w.double().requires_grad_(True)
+    yr = sg3.synthesis_input(sd, inp, wr, dtype=torch.float64)
+    assert (y.detach().cpu().double() - yr.detach()).abs().max().item() < 1e-4 * (1 + yr.abs().max().item())
+    (yr * r.double()).sum().backward()
+    assert _rel(wd.grad, wr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 0.12)])
+def test_synthesis_network_gradient_wrt_ws(cuda, gen256_frozen, precision, tol):
+    """dL/dws through the whole frozen SG3-T-256 synthesis (input, 14 layers, ToRGB, output scale) against
+    torch.autograd through the oracle in fp64; the autograd forward equals the inference forward."""
+    sd = _sd64(gen256_frozen)
+    G = gen256_frozen
+    ws = torch.randn(2, 16, 512, generator=torch.Generator().manual_seed(3)) * 0.7
+    G.set_precision(precision)
+    try:
+        with torch.no_grad():
+            inf = G.synthesis(ws.to(cuda))
+        wd = ws.to(cuda).requires_grad_(True)
+        img = G.synthesis(wd)
+        assert img.grad_fn is not None and img.shape == (2, 3, 256, 256)
+        d_fwd = (img.detach() - inf).abs().max().item()
+        r = torch.randn(img.shape, generator=torch.Generator().manual_seed(6))
+        (img * r.to(cuda)).sum().backward()
+    finally:
+        G.set_precision("fp32")
+    wr = ws.double().requires_grad_(True)
+    ref = sg3.synthesis_forward(sd, 256, wr, dtype=torch.float64)
+    (ref * r.double()).sum().backward()
+    e = _rel(wd.grad, wr.grad)
+    per_ws = [_rel(wd.grad[:, i], wr.grad[:, i]) for i in range(16)]
+    print(f"[synthesis-{precision}] rel grad error {e:.2e}; per ws {[round(v, 5) for v in per_ws]}; "
+          f"|train fwd - inference fwd| {d_fwd:.2e}")
+    assert d_fwd < (1e-4 if precision == "fp32" else 2e-2)
+    assert e < tol
+
+
+def test_synthesis_refuses_weight_gradients(cuda, gen256_frozen):
+    G = gen256_frozen
+    ws = torch.randn(1, 16, 512, device=cuda, requires_grad=True)
+    G.synthesis.L3_52_512.weight.requires_grad_(True)
+    try:
+        with pytest.raises(nv.AutogradUnsupported):
+            G.synthesis(ws)
+    finally:
+        G.synthesis.L3_52_512.weight.requires_grad_(False)
+
+
+ENC64 = dict(img_resolution=64, img_channels=3, w_dim=512, num_ws=16, block_split=(5, 12), channel_base=1024,
+             channel_max=64)
+
+
+def test_compressor_training_loss_gradients(cuda, gen256_frozen):
+    """The reference's training loss (rec MSE + kl_weight * KL to w_avg, ref :669-688; LPIPS excluded) through
+    encoder -> frozen synthesis -> bilinear resize to the training resolution: every encoder gradient against
+    the fp64 oracle chain (oracle encoder with this call's eps and fc1, oracle synthesis, F.interpolate)."""
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(**ENC64).to(cuda)
+    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(9)) * 2 - 1
+    w_avg = torch.randn(1, 1, 512, generator=torch.Generator().manual_seed(10)) * 0.3
+    xd = x.to(cuda)
+    torch.manual_seed(1)
+    wp, m, lv = enc(xd)
+    img = gen256_frozen.synthesis(wp)
+    img = ic2.resize_bilinear(img, (64, 64))
+    loss = F.mse_loss(xd, img) + 0.01 * ict.kl_divergence(m, lv, w_avg.to(cuda))
+    loss.backward()
+    named = dict(enc.named_parameters())
+    sd = {k: v.detach().cpu().double().requires_grad_(True) for k, v in named.items()}
+    eps_all = ((wp - m) / torch.exp(0.5 * lv)).detach().cpu().double()
+    eps = {"global": eps_all[:, :5], "medium": eps_all[:, 5:12], "fine": eps_all[:, 12:]}
+    ow, om, olv = oe.encoder_forward(sd, x.double(), num_ws=16, block_split=(5, 12), w_dim=512,
+                                     fine_fc1=(sd["fine_projector.fc1.weight"], sd["fine_projector.fc1.bias"]), eps=eps)
+    oimg = sg3.synthesis_forward(_sd64(gen256_frozen), 256, ow, dtype=torch.float64)
+    oimg = F.interpolate(oimg, size=(64, 64), mode="bilinear", align_corners=False)
+    oloss = F.mse_loss(x.double(), oimg) + 0.01 * ict.kl_divergence(om, olv, w_avg.double())
+    assert abs(loss.item() - oloss.item()) < 1e-4 * abs(oloss.item())
+    oloss.backward()
+    worst = {}
+    gmax = max(sd[k].grad.norm().item() for k in named if sd[k].grad is not None)
+    for k, p in named.items():
+        if sd[k].grad is None:
+            assert p.grad is None, k
+            continue
+        if sd[k].grad.norm().item() < 1e-8 * gmax:
+            assert p.grad.norm().item() < 1e-4 * gmax, k
+            continue
+        worst[k] = _rel(p.grad, sd[k].grad)
+    print(f"[compressor-train] max relative grad error {max(worst.values()):.2e} over {len(worst)} tensors")
+    assert max(worst.values()) < 1e-3, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+
+
+@pytest.mark.parametrize("second_pass", [True, False])
+def test_train_step_updates_encoder(cuda, gen256_frozen, second_pass):
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(**ENC64).to(cuda)
+    comp = ic2.StyleGAN3Compressor(enc, gen256_frozen, training_resolution=64)
+    opt = ict.make_optimizer(enc, lr=1e-4)
+    x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(cuda)
+    w_avg = gen256_frozen.mapping.w_avg.view(1, 1, -1)
+    before = {k: v.detach().clone() for k, v in enc.named_parameters()}
+    for _ in range(2):
+        out = ict.train_step(comp, x, opt, w_avg, perceptual_weight=0.0, second_encoder_pass=second_pass)
+    vals = {k: v.item() for k, v in out.items()}
+    assert all(np.isfinite(v) for v in vals.values()), vals
+    assert abs(vals["total_loss"] - (vals["rec_loss"] + 0.01 * vals["kl_loss"])) < 1e-5 * vals["total_loss"]
+    changed = [k for k, v in enc.named_parameters() if not torch.equal(v.detach(), before[k])]
+    assert len(changed) >= len(before) // 2, changed
+    assert all(p.grad is None for p in gen256_frozen.parameters())

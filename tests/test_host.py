@@ -64,9 +64,11 @@ def test_forwards_refuse_autograd():
     ws = torch.zeros(1, 16, 512)
     with pytest.raises(nv.AutogradUnsupported):
         G.synthesis(ws)                          # parameters require grad
-    G.requires_grad_(False)
     with pytest.raises(nv.AutogradUnsupported):
-        G.synthesis(ws.requires_grad_(True))     # the input requires grad (grads into W+)
+        G.synthesis(ws.clone().requires_grad_(True))   # weight gradients are not implemented (G is frozen)
+    G.requires_grad_(False)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        G.synthesis(ws.clone().requires_grad_(True))   # frozen G, grads into W+: the HIP autograd path
     with pytest.raises(RuntimeError, match="ROCm"):
         G.synthesis(ws.detach())                 # frozen and no input grad: reaches the device check
     disc = ic2.GumbelSoftmaxDiscretization(32, 256)   # learnable temperature

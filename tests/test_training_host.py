@@ -1,0 +1,107 @@
+"""CPU: host logic of the training path (BASELINE C5) -- the upfirdn2d adjoint padding that every synthesis
+backward uses (checked against torch.autograd through the oracle's upfirdn2d in fp64), the data-parallel
+gradient average over gloo with world size 2, the KL term and the step's argument checks."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from image_compression_2_amd import distributed as icd
+from image_compression_2_amd import training as ict
+from image_compression_2_amd.sg3_ops import upfirdn2d_adjoint_padding
+from oracle import sg3
+
+
+CASES = [  # (h, w, taps, up, down, padding, flip)
+    (12, 12, 12, 2, 1, [7, 6, 7, 6], False),          # an SG3 layer's up-FIR (up 2, 12 taps)
+    (30, 30, 12, 1, 2, 0, False),                      # its down-FIR
+    (9, 11, 24, 4, 1, [13, 11, 14, 10], False),        # up 4
+    (40, 36, 24, 1, 4, 0, True),
+    (10, 10, 5, 2, 2, [1, 3, 2, 0], False),            # up and down at once, odd taps, asymmetric padding
+    (16, 16, 6, 1, 1, [-2, 1, 0, -1], True),           # crops
+    (7, 9, 1, 3, 2, [0, 1, 1, 0], False),              # 1-tap filter
+]
+
+
+@pytest.mark.parametrize("h,w,taps,up,down,pad,flip", CASES)
+def test_upfirdn2d_adjoint_padding_matches_autograd(h, w, taps, up, down, pad, flip):
+    g = torch.Generator().manual_seed(h * 31 + taps)
+    f = torch.rand(taps, generator=g, dtype=torch.float64) + 0.1
+    x = torch.randn(2, 3, h, w, generator=g, dtype=torch.float64, requires_grad=True)
+    gain = float(up * up)
+    y = sg3.upfirdn2d(x, f, up=up, down=down, padding=pad, flip_filter=flip, gain=gain)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (ref,) = torch.autograd.grad(y, x, dy)
+    p = upfirdn2d_adjoint_padding(x.shape[2:], y.shape[2:], f, up, down, pad)
+    got = sg3.upfirdn2d(dy, f, up=down, down=up, padding=p, flip_filter=not flip, gain=gain)
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() < 1e-10 * (1 + ref.abs().max().item())
+
+
+def test_filtered_lrelu_backward_chain_on_oracle_ops():
+    """The chain filtered_lrelu_backward runs (recompute U, adjoint down-FIR, lrelu' * gain with the clamp
+    mask, adjoint up-FIR), restated on the oracle's upfirdn2d, equals autograd of the oracle's filtered_lrelu
+    for an SG3-T layer geometry (up 2, down 2, 12 taps, clamp 256 reached)."""
+    _, layers = sg3.layer_table(256)
+    L = layers[5]
+    g = torch.Generator().manual_seed(5)
+    fu, fd = L["up_filter"].double(), L["down_filter"].double()
+    n, c, s = 2, 4, L["in_size"] + 2
+    z = (torch.randn(n, c, s, s, generator=g, dtype=torch.float64) * 150).requires_grad_(True)
+    y = sg3.filtered_lrelu(z, fu, fd, up=L["up"], down=L["down"], padding=L["padding"], clamp=256)
+    dout = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (ref,) = torch.autograd.grad(y, z, dout)
+    u = sg3.upfirdn2d(z.detach(), fu, up=L["up"], padding=L["padding"], gain=L["up"] ** 2)
+    v = sg3.bias_act(u, act="lrelu", alpha=0.2, gain=np.sqrt(2), clamp=256)
+    assert (v.abs() >= 256).any()
+    m = torch.where(v > 0, np.sqrt(2), 0.2 * np.sqrt(2)) * (v.abs() < 256)
+    pd = upfirdn2d_adjoint_padding(u.shape[2:], dout.shape[2:], fd, 1, L["down"], 0)
+    gv = sg3.upfirdn2d(dout, fd, up=L["down"], padding=pd, flip_filter=True)
+    pu = upfirdn2d_adjoint_padding(z.shape[2:], u.shape[2:], fu, L["up"], 1, L["padding"])
+    got = sg3.upfirdn2d(gv * m, fu, down=L["up"], padding=pu, flip_filter=True, gain=L["up"] ** 2)
+    assert (got - ref).abs().max().item() < 1e-6 * (1 + ref.abs().max().item())
+
+
+def _dp_worker(outq_path):
+    import torch.distributed as dist
+    rank, _, _ = icd.init("gloo")
+    a = torch.nn.Parameter(torch.zeros(5, 3))
+    b = torch.nn.Parameter(torch.zeros(1000))
+    c = torch.nn.Parameter(torch.zeros(7))   # no gradient: skipped on every rank
+    a.grad = torch.full((5, 3), float(rank + 1))
+    b.grad = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+    nb = icd.allreduce_gradients([a, b, c], bucket_bytes=32)   # tiny buckets: one per tensor
+    res = torch.cat([a.grad.reshape(-1), b.grad, torch.tensor([float(nb), float(c.grad is None)])])
+    torch.save(res, f"{outq_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_gradients_gloo_world2(tmp_path):
+    out = str(tmp_path / "dp")
+    icd.launch(2, _dp_worker, out)
+    for r in range(2):
+        res = torch.load(f"{out}.{r}", weights_only=True)
+        assert torch.allclose(res[:15], torch.full((15,), 1.5))
+        assert torch.allclose(res[15:1015], torch.arange(1000, dtype=torch.float32) * 1.5)
+        assert res[1015].item() == 2 and res[1016].item() == 1
+
+
+def test_allreduce_gradients_single_process_is_noop():
+    p = torch.nn.Parameter(torch.ones(3))
+    p.grad = torch.full((3,), 2.0)
+    assert icd.allreduce_gradients([p], world=1) == 0 and p.grad.tolist() == [2.0, 2.0, 2.0]
+
+
+def test_kl_divergence_formula():
+    g = torch.Generator().manual_seed(0)
+    m, lv = torch.randn(3, 16, 8, generator=g), torch.randn(3, 16, 8, generator=g) * 0.3
+    w_avg = torch.randn(1, 1, 8, generator=g)
+    ref = np.mean([0.5 * float(((m[i] - w_avg[0]) ** 2 + lv[i].exp() - lv[i] - 1).sum()) for i in range(3)])
+    assert abs(ict.kl_divergence(m, lv, w_avg).item() - ref) < 1e-5 * abs(ref)
+
+
+def test_train_step_requires_percep_for_perceptual_weight():
+    with pytest.raises(ValueError, match="perceptual"):
+        ict.train_step(None, None, None, None, perceptual_weight=0.8)
