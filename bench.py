@@ -1,6 +1,6 @@
 """Benchmark of the encode -> 8-bit quantize -> synthesize path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--batch B] [--precision bf16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5] [--batch B] [--precision bf16|fp32]
                     [--no-roofline] [--cpu-baseline-images M] [--dry-run]
 
 A step = one pass of the hot path over one synthetic batch already resident in HBM:
@@ -8,6 +8,11 @@ HVAE_VGG_Encoder(img_resolution=1024) on 256^2 images -> 8-bit uniform quantizer
 -> StyleGAN3-T synthesis -> uint8 PSNR sums vs the input -> all_reduce(SUM) of the fp64 metric record.
 Random-init weights of the named architectures (no checkpoints offline), seeded synthetic inputs
 (seed 1000 + rank).
+
+--config c5 (BASELINE config 5, the reference's train_hvae_encoder step, stylegan3_hvae_full.py:655-707): a step
+is one optimisation step of the encoder through the frozen synthesis network (forward, the reference's second
+encoder pass for the KL term, backward, data-parallel gradient all_reduce over RCCL, Adam); LPIPS excluded
+(its pretrained VGG weights are not available offline).
 
 Multi-GPU: one process per GPU, batch-sharded, weak scaling (every rank runs its own batch).  Under torchrun
 the ranks come from the env; `python bench.py --gpus N` without torchrun spawns the N ranks itself
@@ -41,6 +46,8 @@ CONFIGS = {
     # name: (input res, generator res, per-GPU batch, description)
     "c2": (256, 256, 32, "batch=32 256x256 encode+8bit quantize+decode, SG3-T-256 generator"),
     "c4": (1024, 1024, 8, "batch=8 1024x1024 encode+8bit quantize+decode, SG3-T-1024 generator"),
+    "c5": (256, 256, 16, "HVAE encoder training step (rec MSE + 0.01 KL, Adam 1e-4) through frozen SG3-T-256, "
+                         "256x256, per-GPU batch 16, grad all_reduce"),
 }
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA, MI355X_MICROARCH.md
 F32_PEAK_TFLOPS = 157.3     # f32 MFMA / VALU
@@ -101,8 +108,9 @@ class CallTimer:
         return sum(s.elapsed_time(e) for s, e in ev), len(ev)
 
 
-def algorithmic_flops_per_image(enc, G, res):
-    """MFMA-eligible FLOPs per image (unpadded): encoder convs + synthesis input 1x1 + modconvs."""
+def algorithmic_flops_per_image(enc, G, res, split=False):
+    """MFMA-eligible FLOPs per image (unpadded): encoder convs + synthesis input 1x1 + modconvs
+    (split=True -> (encoder, synthesis))."""
     total = 0.0
     h = res
     total += 2 * h * h * enc.from_rgb.out_channels * 9 * enc.from_rgb.in_channels
@@ -112,13 +120,25 @@ def algorithmic_flops_per_image(enc, G, res):
         ci, co = blk.conv1.in_channels, blk.conv1.out_channels
         total += 2 * h * h * co * 9 * ci + 2 * h * h * co * 9 * co
         h = h // 2 if h > 1 else h
+    enc_total = total
     S = int(G.synthesis.input.size[0])
     C = G.synthesis.input.channels
     total += 2 * S * S * C * C
     for L in G.synthesis.layers():
         s = int(L.in_size[0]) + L.conv_kernel - 1
         total += 2 * s * s * L.out_channels * L.conv_kernel ** 2 * L.in_channels
-    return total
+    return (enc_total, total - enc_total) if split else total
+
+
+def training_flops_per_image(enc, G, res):
+    """Conv FLOPs of one c5 step per image: encoder forward twice (the reference's second pass for the KL
+    term), its dgrad (all but from_rgb, whose input needs no gradient) and wgrad; synthesis 1x1 input mix in
+    torch, its modulated convs forward + dgrad."""
+    e, s = algorithmic_flops_per_image(enc, G, res, split=True)
+    rgb = 2 * res * res * enc.from_rgb.out_channels * 9 * enc.from_rgb.in_channels
+    S, C = int(G.synthesis.input.size[0]), G.synthesis.input.channels
+    s_mod = s - 2 * S * S * C * C
+    return 2 * e + (e - rgb) + e + 2 * s_mod
 
 
 def algorithmic_bytes_per_image(enc, G, res, esz):
@@ -232,6 +252,36 @@ def cpu_baseline(res, gen_res, n_images):
                        f"B=1 / B=32 / 1024^2 rows: profiles/r2_cpu_baseline.json")
 
 
+def cpu_baseline_train(res, gen_res, n_images):
+    """The oracle's fp32 CPU restatement of one c5 training step on n_images: encoder forward (x2, as the
+    reference), synthesis forward, rec MSE + 0.01 KL, backward into the encoder's parameters."""
+    from oracle import encoder as oe
+    from oracle import sg3
+    import image_compression_2_amd as ic2
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024)
+    sd_e = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()}
+    sd_g = sg3.init_params(gen_res, seed=1)
+    x = torch.rand(n_images, 3, res, res, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+    torch.manual_seed(5)
+    lin = torch.nn.Linear(128, 256)
+    fc1 = (lin.weight.detach(), lin.bias.detach())
+    w_avg = torch.zeros(1, 1, 512)
+    t0 = time.perf_counter()
+    w, _, _ = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
+    img = sg3.synthesis_forward(sd_g, gen_res, w)
+    _, m, lv = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
+    kl = 0.5 * torch.mean(torch.sum((m - w_avg) ** 2 + lv.exp() - lv - 1, dim=[1, 2]))
+    loss = torch.nn.functional.mse_loss(x, img) + 0.01 * kl
+    loss.backward()
+    dt = time.perf_counter() - t0
+    return dict(value=round(n_images / dt, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
+                cpu_model=cpu_model(),
+                sample=f"{n_images} image(s) {res}x{res}: encoder(1024-config) fwd x2 + SG3-T-{gen_res} synthesis fwd "
+                       f"+ MSE/KL + backward, fp32 autograd over the oracle/ restatement on {torch.get_num_threads()} "
+                       f"threads, {dt:.1f} s")
+
+
 # ------------------------------------------------------------------------------------------------
 def timed_loop(step, steps, sync, barrier, use_events):
     """Barrier + sync, EXACTLY `steps` steps, sync + barrier + sync.  -> (last output, wall s, per-step ms)."""
@@ -292,13 +342,27 @@ def run(args):
         import image_compression_2_amd as ic2
         from image_compression_2_amd import _native as nv
         from image_compression_2_amd import metrics as icm
+        train = args.config == "c5"
         torch.manual_seed(0)
-        enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=args.precision).to(dev).eval().requires_grad_(False)
+        enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=args.precision).to(dev)
+        if not train:
+            enc.eval().requires_grad_(False)
         torch.manual_seed(1)
         G = ic2.Generator(img_resolution=gen_res, precision=args.precision).to(dev).eval()
-        comp = ic2.StyleGAN3Compressor(enc, G)
+        comp = ic2.StyleGAN3Compressor(enc, G, training_resolution=res if train else None)
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         x = torch.rand(batch, 3, res, res, generator=g, device=dev) * 2 - 1
+
+        if train:
+            from image_compression_2_amd import training as ict
+            opt = ict.make_optimizer(enc, lr=1e-4)
+            w_avg = G.mapping.w_avg.view(1, 1, -1)
+
+            def train_step():
+                losses = ict.train_step(comp, x, opt, w_avg, rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01)
+                vec = torch.stack([losses["rec_loss"].double() * batch, losses["kl_loss"].double() * batch,
+                                   torch.tensor(float(batch), device=dev, dtype=torch.float64)])
+                return icd.allreduce_sum(vec, device=dev)
 
         def step():
             with torch.no_grad():
@@ -309,6 +373,8 @@ def run(args):
                                torch.tensor(float(batch), device=dev, dtype=torch.float64)])
             return icd.allreduce_sum(vec, device=dev)
 
+    if not dry and args.config == "c5":
+        step = train_step
     for _ in range(args.warmup):
         step()
     vec, elapsed, per_step = timed_loop(step, args.steps, sync, barrier, use_events=not dry)
@@ -321,8 +387,10 @@ def run(args):
     total_images = batch * args.steps * world
     value = total_images / elapsed_max
     vec = vec.cpu()
+    metric = {"c2": "images/sec encode+decode 256px", "c4": "images/sec encode+decode 1024px",
+              "c5": "images/sec encoder training step 256px"}[args.config]
     out = {
-        "metric": "images/sec encode+decode 256px" if args.config == "c2" else "images/sec encode+decode 1024px",
+        "metric": metric,
         "value": round(value, 3),
         "unit": "images/s",
         "n_gpus": world,
@@ -346,11 +414,37 @@ def run(args):
     if dry:
         out["dry_run"] = True
         out["psnr_db_record"] = float(10 * torch.log10(255.0 ** 2 / (vec[0] / vec[1])))
+    elif args.config == "c5":
+        out["config"].update(quantization_bits=None, loss="rec MSE + 0.01 KL(w_avg); LPIPS excluded (no weights "
+                             "offline)", optimizer="Adam(1e-4, (0.9, 0.999))",
+                             parallelism=f"dp{world} (batch-sharded, RCCL gradient all_reduce)")
+        out["last_step_losses"] = {"rec_loss": round(vec[0].item() / vec[2].item(), 6),
+                                   "kl_loss": round(vec[1].item() / vec[2].item(), 4)}
     else:
         from image_compression_2_amd import metrics as icm
         out["psnr_db_vs_input"] = round(icm.psnr_from_sums(vec[0].item(), vec[1].item()), 4)
 
-    if not dry and not args.no_roofline:
+    if not dry and not args.no_roofline and args.config == "c5":
+        names = ("ic2_conv_igemm", "ic2_conv_igemm_ws", "ic2_conv_wgrad")
+        timer = CallTimer(nv, names)
+        timer.install()
+        timer.enabled = True
+        n_inst = min(args.steps, 5)
+        timed_loop(step, n_inst, sync, barrier, use_events=True)
+        timer.enabled = False
+        timer.uninstall()
+        conv_ms, n_launch = timer.total(names)
+        flops_img = training_flops_per_image(enc, G, res)
+        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
+        achieved = flops_img * batch * n_inst / (conv_ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "ic2 conv family forward + dgrad (implicit GEMM) + wgrad",
+                           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(achieved / peak, 4), "traffic": None, "launches": n_launch,
+                           "avg_launch_ms": round(conv_ms / max(n_launch, 1), 4),
+                           "conv_ms_per_step": round(conv_ms / n_inst, 3),
+                           "path_frac": round(value / world * flops_img / (peak * 1e12), 4),
+                           "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}
+    elif not dry and not args.no_roofline:
         conv_names = ("ic2_conv_igemm", "ic2_conv_igemm_ws")
         timer = CallTimer(nv, conv_names + ("ic2_flrelu_nhwc",))
         timer.install()
@@ -390,7 +484,9 @@ def run(args):
                 "achieved_tflops": round(f_img * batch / (flr_step * 1e-3) / 1e12, 2),
                 "achieved_gbs": round(b_img * batch / (flr_step * 1e-3) / 1e9, 1), "launches": n_flr}
 
-    if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
+    if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry and args.config == "c5":
+        out["cpu_baseline"] = cpu_baseline_train(res, gen_res, 1)
+    elif rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
         out["cpu_baseline"] = cpu_baseline(res if args.config == "c2" else 256, gen_res if args.config == "c2" else 256,
                                            args.cpu_baseline_images)
     if rank == 0:

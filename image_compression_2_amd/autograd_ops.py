@@ -20,11 +20,13 @@ their styles only:
 
     modulated conv (SG3 modulated_conv2d)  fwd ic2_conv_igemm (normalised W)   bwd dx: ic2_conv_igemm on the
                                                                                  flipped, transposed W
-    filtered lrelu (SG3 filtered_lrelu)    fwd ic2_flrelu_nhwc                bwd recompute up(z); adjoint
-                                                                                 FIRs via ic2_upfirdn2d
+    filtered lrelu (SG3 filtered_lrelu)    fwd ic2_flrelu_nhwc                bwd ic2_flrelu_bwd_nhwc (fused:
+                                                                                 recompute up(z), adjoint FIRs)
     styles / (de)modulation / Fourier input    torch ops on [N, <= 512] rows and the 36x36 input grid
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
@@ -206,11 +208,18 @@ def _flr_chunk(n, c, hu, wu):
 
 class FilteredLReluNHWC(torch.autograd.Function):
     """SG3 filtered_lrelu on NHWC activations with the layer's filters, padding, gain sqrt(2), slope 0.2 and
-    clamp (SynthesisLayer.forward).  Forward: the fused HIP kernel.  Backward: per chunk of samples, NCHW f32
-    planes of the valid channels through sg3_ops.filtered_lrelu_backward (HIP upfirdn2d kernels)."""
+    clamp (SynthesisLayer.forward).  y arrives in f32; in bf16 mode it is saturated to the f16 range and stored
+    as f16 for the MFMA forward kernel (the inference epilogue's semantics), and that f16 copy is what the
+    backward recomputes from.  Forward: the fused HIP kernel.  Backward: ic2_flrelu_bwd_nhwc (one fused HIP
+    kernel: U recompute, adjoint down-FIR, lrelu'/clamp mask, adjoint up-FIR; f32 gradient) for the StyleGAN3-T
+    geometries, otherwise per chunk of samples through sg3_ops.filtered_lrelu_backward (HIP upfirdn2d)."""
 
     @staticmethod
     def forward(ctx, y, layer, dt_out):
+        if dt_out == torch.bfloat16:
+            y = y.clamp(-65504.0, 65504.0).to(torch.float16)
+        else:
+            y = y.contiguous()
         out = layer.flrelu_nhwc(y, dt_out)
         ctx.save_for_backward(y)
         ctx.layer = layer
@@ -218,20 +227,40 @@ class FilteredLReluNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        from . import sg3_ops
         (y,) = ctx.saved_tensors
         L = ctx.layer
+        dout = dout.contiguous()
         n, h, w, c_p = y.shape
-        c = L.out_channels
-        dy = torch.zeros_like(y)
-        hu = h * L.up_factor + L.padding[2] + L.padding[3] - (L.up_taps - 1)
-        wu = w * L.up_factor + L.padding[0] + L.padding[1] - (L.up_taps - 1)
-        step = _flr_chunk(n, c, hu, wu)
-        clamp = float(L.conv_clamp) if L.conv_clamp is not None else None
-        for i in range(0, n, step):
-            z = y[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
-            g = dout[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
-            dz = sg3_ops.filtered_lrelu_backward(z, g, L.up_filter, L.down_filter, L.up_factor, L.down_factor,
-                                                 L.padding, L.act_gain, 0.2, clamp)
-            dy[i:i + step, :, :, :c] = dz.permute(0, 2, 3, 1).to(y.dtype)
-        return dy, None, None
+        fu, fd = L._fu, L._fd
+        px0, px1, py0, py1 = L.padding
+        clamp = float(L.conv_clamp) if L.conv_clamp is not None else -1.0
+        if fu is not None and fd is not None and px0 == py0:
+            dy = torch.empty([n, h, w, c_p], dtype=torch.float32, device=y.device)
+            rc = nv.load().ic2_flrelu_bwd_nhwc(
+                nv.ptr(y), nv.dtype_code(y.dtype), nv.ptr(dout), nv.dtype_code(dout.dtype), nv.ptr(dy), n, c_p, h, w,
+                dout.shape[1], dout.shape[2], fu.ctypes.data_as(ctypes.c_void_p), fu.shape[0],
+                fd.ctypes.data_as(ctypes.c_void_p), fd.shape[0], L.up_factor, L.down_factor, px0, px1, py0, py1,
+                float(L.act_gain), 0.2, clamp, 0, nv.stream_of(y))
+            if rc == 0:
+                return dy, None, None
+            if rc != 2:   # anything but IC2_E_UNSUPPORTED is an error
+                raise RuntimeError(f"ic2_flrelu_bwd_nhwc failed: {nv.load().ic2_last_error().decode()}")
+        return _flrelu_backward_composed(y, dout, L), None, None
+
+
+def _flrelu_backward_composed(y, dout, L):
+    from . import sg3_ops
+    n, h, w, c_p = y.shape
+    c = L.out_channels
+    dy = torch.zeros([n, h, w, c_p], dtype=torch.float32, device=y.device)
+    hu = h * L.up_factor + L.padding[2] + L.padding[3] - (L.up_taps - 1)
+    wu = w * L.up_factor + L.padding[0] + L.padding[1] - (L.up_taps - 1)
+    step = _flr_chunk(n, c, hu, wu)
+    clamp = float(L.conv_clamp) if L.conv_clamp is not None else None
+    for i in range(0, n, step):
+        z = y[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
+        g = dout[i:i + step, :, :, :c].permute(0, 3, 1, 2).float().contiguous()
+        dz = sg3_ops.filtered_lrelu_backward(z, g, L.up_filter, L.down_filter, L.up_factor, L.down_factor,
+                                             L.padding, L.act_gain, 0.2, clamp)
+        dy[i:i + step, :, :, :c] = dz.permute(0, 2, 3, 1)
+    return dy

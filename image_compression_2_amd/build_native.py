@@ -34,7 +34,9 @@ def _newer(src_paths, target):
 
 # per-file extras: the MFMA filtered-lrelu consumes every accumulator with VALU, so its MFMAs write VGPRs
 # directly instead of AGPRs (saves one v_accvgpr_read per value)
-FILE_FLAGS = {"flrelu_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"flrelu_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+              # the backward FIR loops must unroll fully (register-resident taps; no scratch, no LDS promotion)
+              "flrelu_bwd.hip": ["-mllvm", "-pragma-unroll-threshold=200000"]}
 
 
 def _compile(src, headers, force):

@@ -421,9 +421,6 @@ class SynthesisLayer(torch.nn.Module):
                 y = y.clamp(-float(self.conv_clamp), float(self.conv_clamp))
             img = y[..., : self.out_channels].permute(0, 3, 1, 2)
             return img if final_scale is None else img * float(final_scale)
-        if dt == torch.bfloat16:
-            # the MFMA filtered lrelu takes f16 operands; the inference epilogue saturates at the f16 range
-            y = y.clamp(-65504.0, 65504.0).to(torch.float16)
         return ao.FilteredLReluNHWC.apply(y, self, dt)
 
     def forward(self, x, w, noise_mode="random", force_fp32=False, update_emas=False):

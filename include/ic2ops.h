@@ -235,6 +235,17 @@ int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y
 /* Backward of ic2_global_avg_pool (AdaptiveAvgPool2d(1), :218): dx [n][hw][c_p] = dpooled [n][c] / hw. */
 int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_p, int c, void* stream);
 
+/* Backward of ic2_flrelu_nhwc w.r.t. its input (SynthesisLayer's filtered_lrelu, SG3-public; the encoder's loss
+ * reaches W+ through it, :669-696): x = the forward's input (NHWC [n][in_h][in_w][c_p], f32 or f16), gout = the
+ * gradient of its output (NHWC [n][out_h][out_w][c_p], f32 or bf16) -> gx (NHWC, f32).  Recomputes the upsampled
+ * pre-activation, masks the adjoint down-FIR by lrelu' * gain (zero where clamped) and applies the adjoint up-FIR.
+ * fu / fd: HOST taps.  StyleGAN3-T geometries (up 2 / 4 with 6*up taps, down 2 with 12 taps, px0 == py0); other
+ * configurations return IC2_E_UNSUPPORTED (the caller composes ic2_upfirdn2d then). */
+int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout, int g_dtype, float* gx, int n, int c_p, int in_h,
+                        int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps,
+                        int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
+                        int flip, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

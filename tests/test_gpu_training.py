@@ -365,3 +365,35 @@ def test_train_step_updates_encoder(cuda, gen256_frozen, second_pass):
     changed = [k for k, v in enc.named_parameters() if not torch.equal(v.detach(), before[k])]
     assert len(changed) >= len(before) // 2, changed
     assert all(p.grad is None for p in gen256_frozen.parameters())
+
+
+@pytest.mark.parametrize("li", [2, 5, 9, 12])
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_flrelu_backward_kernel(cuda, gen256_frozen, li, mode):
+    """ic2_flrelu_bwd_nhwc (fused: U recompute, adjoint down-FIR, lrelu'/clamp mask, adjoint up-FIR) on the
+    SG3-T-256 layer geometries (up 2 and 4, the layers' crop / pad offsets) against autograd through the
+    oracle's filtered_lrelu in fp64 on the same stored operands (bf16 mode: f16 input, bf16 output gradient).
+    Clamp reached on a third of the channels."""
+    L = gen256_frozen.synthesis.layers()[li]
+    c, cp = L.out_channels, L.cout_p
+    s = int(L.in_size[0]) + L.conv_kernel - 1
+    g = torch.Generator().manual_seed(li)
+    y = torch.randn(1, s, s, c, generator=g) * 3
+    y[..., : c // 3] = y[..., : c // 3] * 60 + 150
+    y = F.pad(y, (0, cp - c))
+    dt = torch.float32 if mode == "fp32" else torch.bfloat16
+    yd = y.to(cuda).requires_grad_(True)
+    out = ao.FilteredLReluNHWC.apply(yd, L, dt)
+    gout = F.pad(torch.randn(out.shape[:3] + (c,), generator=g), (0, cp - c)).to(dt)
+    out.backward(gout.to(cuda))
+    yr = (y if mode == "fp32" else y.half().float()).double()[..., :c].permute(0, 3, 1, 2).requires_grad_(True)
+    _, layers = sg3.layer_table(256)
+    Lr = layers[li]
+    o = sg3.filtered_lrelu(yr, Lr["up_filter"].double(), Lr["down_filter"].double(), up=Lr["up"], down=Lr["down"],
+                           padding=Lr["padding"], clamp=256)
+    o.backward(gout.double()[..., :c].permute(0, 3, 1, 2))
+    got = yd.grad.float().cpu()
+    assert got.dtype == torch.float32 and (c == cp or got[..., c:].abs().max().item() == 0.0)
+    e = _rel(got[..., :c].permute(0, 3, 1, 2), yr.grad)
+    print(f"[flrelu-bwd L{li} {mode}] rel err {e:.2e}")
+    assert e < 1e-3
