@@ -46,6 +46,9 @@ CONFIGS = {
     # name: (input res, generator res, per-GPU batch, description)
     "c2": (256, 256, 32, "batch=32 256x256 encode+8bit quantize+decode, SG3-T-256 generator"),
     "c4": (1024, 1024, 8, "batch=8 1024x1024 encode+8bit quantize+decode, SG3-T-1024 generator"),
+    # reading (ii) of the 256^2 configs: the reference's default 1024 generator, its output bilinearly
+    # decimated to the 256^2 input (StyleGAN3Compressor.forward, stylegan3_hvae_full.py:277-279)
+    "c2r": (256, 1024, 32, "batch=32 256x256 encode+8bit quantize+decode on SG3-T-1024, bilinear decimation to 256"),
     "c5": (256, 256, 16, "HVAE encoder training step (rec MSE + 0.01 KL, Adam 1e-4) through frozen SG3-T-256, "
                          "256x256, per-GPU batch 16, grad all_reduce"),
 }
@@ -243,11 +246,14 @@ def cpu_baseline(res, gen_res, n_images):
     with torch.no_grad():
         _, m, _ = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
         q = oe.quantize_uniform(m, 8)
-        sg3.synthesis_forward(sd_g, gen_res, q)
+        img = sg3.synthesis_forward(sd_g, gen_res, q)
+        if img.shape[2] != res:
+            torch.nn.functional.interpolate(img, size=(res, res), mode="bilinear", align_corners=False)
     dt = time.perf_counter() - t0
     return dict(value=round(n_images / dt, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
                 cpu_model=cpu_model(),
                 sample=f"{n_images} image(s) {res}x{res}, encoder(1024-config) + 8-bit quantize + SG3-T-{gen_res} "
+                       f"{'(+ bilinear decimation) ' if gen_res != res else ''}"
                        f"synthesis, fp32, oracle/ restatement on {torch.get_num_threads()} threads, {dt:.1f} s; "
                        f"B=1 / B=32 / 1024^2 rows: profiles/r2_cpu_baseline.json")
 
@@ -368,6 +374,8 @@ def run(args):
             with torch.no_grad():
                 q = comp.compress(x, quantization_bits=8, deterministic=True)
                 img = comp.decompress(q)
+                if img.shape[2] != res:
+                    img = ic2.resize_bilinear(img, (res, res))
                 sse = icm.uint8_sse(img, x)
             vec = torch.stack([sse.sum(), torch.tensor(float(img.numel()), device=dev, dtype=torch.float64),
                                torch.tensor(float(batch), device=dev, dtype=torch.float64)])
@@ -388,6 +396,7 @@ def run(args):
     value = total_images / elapsed_max
     vec = vec.cpu()
     metric = {"c2": "images/sec encode+decode 256px", "c4": "images/sec encode+decode 1024px",
+              "c2r": "images/sec encode+decode 256px (1024 generator, decimated)",
               "c5": "images/sec encoder training step 256px"}[args.config]
     out = {
         "metric": metric,
@@ -487,8 +496,11 @@ def run(args):
     if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry and args.config == "c5":
         out["cpu_baseline"] = cpu_baseline_train(res, gen_res, 1)
     elif rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
-        out["cpu_baseline"] = cpu_baseline(res if args.config == "c2" else 256, gen_res if args.config == "c2" else 256,
-                                           args.cpu_baseline_images)
+        if args.config == "c2r":
+            out["cpu_baseline"] = cpu_baseline(res, gen_res, 1)
+        else:
+            out["cpu_baseline"] = cpu_baseline(res if args.config == "c2" else 256,
+                                               gen_res if args.config == "c2" else 256, args.cpu_baseline_images)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

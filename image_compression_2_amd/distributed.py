@@ -108,7 +108,7 @@ def barrier(device=None):
 
 def allreduce_gradients(params, world=None, bucket_bytes=64 << 20):
     """Average the .grad of ``params`` over ranks in place: grads are packed into flat f32 buckets of about
-    ``bucket_bytes`` (one all_reduce per bucket: the encoder's ~26 M gradients are two RCCL calls, large
+    ``bucket_bytes`` (one all_reduce per bucket: the encoder's 37.5 M gradients are three RCCL calls, large
     enough to run at xGMI ring bandwidth) and copied back divided by the world size.  Parameters without a
     gradient are skipped; every rank runs the same module graph, so the bucket layout agrees across ranks."""
     if world is None:
