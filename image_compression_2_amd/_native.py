@@ -66,12 +66,21 @@ _SIGS = {
     "ic2_gn_lrelu_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _I64,
                               _P],
     "ic2_gap_bwd": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "ic2_flrelu_bwd_ydot_floats": [_I, _I, _I, _I, _I],
+    "ic2_flrelu_bwd_nhwc_ex": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
+                               _F, _F, _F, _I, _P, _P, _P, _I64, _P],
+    "ic2_scale_bwd_part_floats": [_I, _I, _I],
+    "ic2_scale_bwd_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I64, _P],
+    "ic2_conv3x3_gn_stats_floats": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
+    "ic2_conv3x3_gn_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _I64, _P, _I64, _I,
+                           _P],
     "ic2_flrelu_bwd_nhwc": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F,
                             _F, _I, _P],
 }
 _RESTYPE = {"ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
             "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64, "ic2_conv_wgrad_ws_floats": _I64,
-            "ic2_gn_lrelu_pool_bwd_floats": _I64}
+            "ic2_gn_lrelu_pool_bwd_floats": _I64, "ic2_conv3x3_gn_stats_floats": _I64,
+            "ic2_flrelu_bwd_ydot_floats": _I64, "ic2_scale_bwd_part_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()

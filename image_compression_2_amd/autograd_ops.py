@@ -264,3 +264,76 @@ def _flrelu_backward_composed(y, dout, L):
                                              L.padding, L.act_gain, 0.2, clamp)
         dy[i:i + step, :, :, :c] = dz.permute(0, 2, 3, 1)
     return dy
+
+
+class SynthLayerNHWC(torch.autograd.Function):
+    """One non-ToRGB synthesis layer on the autograd path, w.r.t. its input activation and its (de)modulation
+    coefficients (SG3 SynthesisLayer.forward with frozen weights):
+        a = x * xscale[n][i]  ->  y = conv(a, W_norm) * oscale[n][o] + bias  ->  out = filtered_lrelu(y)
+    Forward = the inference kernels (ic2_conv_igemm with oscale / bias / f16-saturating epilogue in bf16 mode,
+    ic2_flrelu_nhwc).  Backward, three HIP launches:
+        ic2_flrelu_bwd_nhwc_ex  dL/dy (FLR adjoint), stored times oscale (= dL/dconv, the dgrad operand) and the
+                                per-tile sums of dL/dy * (y - bias) -> dL/doscale = sum / oscale
+        ic2_conv_igemm          dL/da = conv(dL/dconv, flipped / transposed W)
+        ic2_scale_bwd_nhwc      dL/dx = dL/da * xscale, dL/dxscale = sum_p dL/da * x"""
+
+    @staticmethod
+    def forward(ctx, x, xs, os_, layer, dt):
+        n, s_in = x.shape[0], x.shape[1]
+        a = x * xs[:, None, None, :].to(x.dtype)
+        k = layer.conv_kernel
+        pad = k - 1
+        conv = s_in + 2 * pad - k + 1
+        wp, _, bp = layer.packed(dt)
+        ydt = torch.float16 if dt == torch.bfloat16 else dt
+        y = torch.empty([n, conv, conv, layer.cout_p], dtype=ydt, device=x.device)
+        nv.conv_igemm(nv.ptr(a), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
+                      layer.cin_p, layer.cout_p, layer.out_channels, k, k, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0,
+                      0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(x), x.device)
+        del a
+        out = layer.flrelu_nhwc(y, dt)
+        ctx.save_for_backward(x, xs, os_, y)
+        ctx.layer, ctx.dt = layer, dt
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, xs, os_, y = ctx.saved_tensors
+        L, dt = ctx.layer, ctx.dt
+        dout = dout.contiguous()
+        n, h, w, c_p = y.shape
+        stream = nv.stream_of(y)
+        _, _, bp = L.packed(dt)
+        fu, fd = L._fu, L._fd
+        px0, px1, py0, py1 = L.padding
+        clamp = float(L.conv_clamp) if L.conv_clamp is not None else -1.0
+        dc = torch.empty([n, h, w, c_p], dtype=dt, device=y.device)
+        rc = 2
+        if fu is not None and fd is not None and px0 == py0:
+            nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, c_p, h, w, L.up_factor))
+            ydot = torch.empty([nyd], dtype=torch.float32, device=y.device)
+            rc = nv.load().ic2_flrelu_bwd_nhwc_ex(
+                nv.ptr(y), nv.dtype_code(y.dtype), nv.ptr(dout), nv.dtype_code(dout.dtype), nv.ptr(dc),
+                nv.dtype_code(dt), n, c_p, h, w, dout.shape[1], dout.shape[2], fu.ctypes.data_as(ctypes.c_void_p),
+                fu.shape[0], fd.ctypes.data_as(ctypes.c_void_p), fd.shape[0], L.up_factor, L.down_factor, px0, px1,
+                py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(os_), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
+            if rc not in (0, 2):
+                raise RuntimeError(f"ic2_flrelu_bwd_nhwc_ex failed: {nv.load().ic2_last_error().decode()}")
+        if rc == 0:
+            yd = ydot.view(n, -1, c_p).sum(1)
+        else:   # no fused instance for this geometry: the composed HIP path + torch epilogue
+            gy = _flrelu_backward_composed(y, dout, L)
+            dc.copy_(gy * os_[:, None, None, :])
+            yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
+        d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
+        # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1)
+        da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0)
+        del dc
+        n_, hi, wi, cin_p = x.shape
+        npart = int(nv.query("ic2_scale_bwd_part_floats", n, hi * wi, cin_p))
+        part = torch.empty([npart], dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        nv.call("ic2_scale_bwd_nhwc", nv.ptr(da), nv.ptr(x), nv.ptr(xs), nv.ptr(dx), nv.dtype_code(x.dtype), n, hi * wi,
+                cin_p, nv.ptr(part), npart, stream)
+        d_xs = part.view(n, -1, cin_p).sum(1)
+        return dx, d_xs, d_os, None, None

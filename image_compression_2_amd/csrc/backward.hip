@@ -338,9 +338,95 @@ static unsigned grid_for(int64_t total) {
   return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Backward of the synthesis layers' input modulation a = x * xscale[n][c] (SG3 modulated_conv2d's style
+// multiply in activation-scaling form): dx = da * xscale, and d xscale[n][c] = sum_p da * x as per-chunk partial
+// sums (fixed order; the host sums the chunks).  Block = (sample, pixel chunk); threads own channel pairs.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline int sb_chunk_pix(int n, int hw) {
+  const int64_t want = ceil_div((int64_t)n * hw, 2048);
+  return (int)(want < 16 ? 16 : (want > 1024 ? 1024 : want));
+}
+
+template <typename T> __device__ __forceinline__ float2 sb_ld2(const T* p);
+template <> __device__ __forceinline__ float2 sb_ld2<float>(const float* p) { return *reinterpret_cast<const float2*>(p); }
+template <> __device__ __forceinline__ float2 sb_ld2<bf16_t>(const bf16_t* p) {
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
+}
+template <typename T> __device__ __forceinline__ void sb_st2(T* p, float2 v);
+template <> __device__ __forceinline__ void sb_st2<float>(float* p, float2 v) { *reinterpret_cast<float2*>(p) = v; }
+template <> __device__ __forceinline__ void sb_st2<bf16_t>(bf16_t* p, float2 v) {
+  *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) scale_bwd_kernel(const T* __restrict__ da, const T* __restrict__ x,
+                                                        const float* __restrict__ xs, T* __restrict__ dx,
+                                                        float* __restrict__ part, int hw, int c_p, int nchunks,
+                                                        int chunk_pix) {
+  extern __shared__ __attribute__((aligned(16))) float sbred[];  // [PS][c_p]
+  const int chunk = blockIdx.x % nchunks;
+  const int nn = blockIdx.x / nchunks;
+  const int npair = c_p >> 1;
+  const int CT = npair < 256 ? npair : 256;
+  const int PS = 256 / CT;
+  const int cq0 = threadIdx.x % CT, pp = threadIdx.x / CT;
+  const int p0 = chunk * chunk_pix, p1 = min(hw, p0 + chunk_pix);
+  const int64_t base = (int64_t)nn * hw * c_p;
+  if (pp < PS) {
+    for (int cq = cq0; cq < npair; cq += CT) {
+      const float2 sc = *reinterpret_cast<const float2*>(xs + (int64_t)nn * c_p + 2 * cq);
+      float s0 = 0.f, s1 = 0.f;
+      for (int p = p0 + pp; p < p1; p += PS) {
+        const int64_t e = base + (int64_t)p * c_p + 2 * cq;
+        const float2 g = sb_ld2(da + e), v = sb_ld2(x + e);
+        s0 += g.x * v.x;
+        s1 += g.y * v.y;
+        sb_st2(dx + e, make_float2(g.x * sc.x, g.y * sc.y));
+      }
+      sbred[pp * c_p + 2 * cq] = s0;
+      sbred[pp * c_p + 2 * cq + 1] = s1;
+    }
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < c_p; ch += 256) {
+    float t = 0.f;
+    for (int k = 0; k < PS; ++k) t += sbred[k * c_p + ch];
+    part[((int64_t)nn * nchunks + chunk) * c_p + ch] = t;
+  }
+}
+
 }  // namespace ic2
 
 using namespace ic2;
+
+extern "C" int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p) {
+  if (n <= 0 || hw <= 0 || c_p <= 0) return 0;
+  return (int64_t)n * ceil_div(hw, sb_chunk_pix(n, hw)) * c_p;
+}
+
+extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw,
+                                  int c_p, float* part, int64_t part_floats, void* stream) {
+  IC2_CHECK_ARG(da && x && xscale && dx && part && n > 0 && hw > 0 && c_p > 0 && c_p % 2 == 0 && c_p <= 512,
+                "scale_bwd_nhwc: bad arguments");
+  IC2_CHECK_ARG(part_floats >= ic2_scale_bwd_part_floats(n, hw, c_p), "scale_bwd_nhwc: partial buffer too small");
+  const int chunk_pix = sb_chunk_pix(n, hw);
+  const int nchunks = (int)ceil_div(hw, chunk_pix);
+  const int npair = c_p / 2, CT = npair < 256 ? npair : 256, PS = 256 / CT;
+  const size_t lds = (size_t)PS * c_p * sizeof(float);
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(scale_bwd_kernel<float>, dim3(n * nchunks), dim3(256), lds, s, (const float*)da, (const float*)x,
+                       xscale, (float*)dx, part, hw, c_p, nchunks, chunk_pix);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(scale_bwd_kernel<bf16_t>, dim3(n * nchunks), dim3(256), lds, s, (const bf16_t*)da,
+                       (const bf16_t*)x, xscale, (bf16_t*)dx, part, hw, c_p, nchunks, chunk_pix);
+  else
+    IC2_CHECK_ARG(false, "scale_bwd_nhwc: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("scale_bwd_nhwc");
+  return IC2_OK;
+}
 
 extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad) {
   WgradArgs a{};

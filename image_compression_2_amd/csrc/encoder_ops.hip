@@ -424,6 +424,13 @@ __global__ void __launch_bounds__(256) resize_bilinear_kernel(const float* __res
   }
 }
 
+// igemm.hip: the conv with the GroupNorm partial sums fused into the halo conv's epilogue
+int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
+                  int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
+                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s);
+int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
+                                   int groups);
+
 }  // namespace ic2
 
 using namespace ic2;
@@ -489,6 +496,43 @@ extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups,
                      nchunks, (double)hw * (c / groups), eps, stats_out);
   IC2_CHECK_LAUNCH("group_norm_stats");
+  return IC2_OK;
+}
+
+extern "C" int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
+                                               int pad, int groups) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (n <= 0 || ho <= 0 || wo <= 0 || groups <= 0) return 0;
+  const int64_t sep = ic2_group_norm_stats_floats(n, ho * wo, groups);
+  const int64_t stats_floats = ((int64_t)n * groups * 2 + 1) / 2 * 2;
+  const int64_t fused = stats_floats + 2 * conv_gn_fused_part_doubles(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad, groups);
+  return sep > fused ? sep : fused;
+}
+
+// VGGBlock conv (+ bias) and the GroupNorm statistics of its output.  When the halo
+// conv runs the layer, the per-tile (sum, sumsq) come out of its epilogue (no second read of y); otherwise the
+// separate two-stage statistics pass runs.  stats: ic2_conv3x3_gn_stats_floats() floats; the first n*groups*2 are
+// (mean, rstd) per (sample, group), as ic2_group_norm_stats writes them.
+extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
+                                  int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, int groups,
+                                  float eps, float* stats, int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes,
+                                  int fuse, void* stream) {
+  IC2_CHECK_ARG(x && w && y && stats && groups > 0 && cout_valid > 0 && cout_valid % groups == 0,
+                "conv3x3_gn_fwd: bad arguments");
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  IC2_CHECK_ARG(stats_floats >= ic2_conv3x3_gn_stats_floats(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad, groups),
+                "conv3x3_gn_fwd: stats buffer too small");
+  hipStream_t s = as_stream(stream);
+  const int64_t sf = ((int64_t)n * groups * 2 + 1) / 2 * 2;
+  double* part = reinterpret_cast<double*>(stats + sf);
+  const int nch = conv_gn_fused(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, part,
+                                (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s);
+  if (nch < 0) return IC2_E_INVALID;
+  if (nch == 0)
+    return ic2_group_norm_stats(y, dtype, n, ho * wo, cout_p, cout_valid, groups, eps, stats, stream);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups, nch,
+                     (double)ho * wo * (cout_valid / groups), eps, stats);
+  IC2_CHECK_LAUNCH("conv3x3_gn_fwd");
   return IC2_OK;
 }
 

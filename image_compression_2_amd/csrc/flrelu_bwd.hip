@@ -31,7 +31,11 @@ typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
 struct FlrBwdArgs {
   const void* x;     // conv output that fed the forward (NHWC [n][in_h][in_w][c_p], f32 or f16)
   const void* gout;  // gradient of the layer output (NHWC [n][out_h][out_w][c_p], f32 or bf16)
-  float* gx;         // gradient of x (NHWC, f32)
+  void* gx;          // gradient of x (NHWC, f32; or bf16 when out_bf16), times oscale[n][c] when oscale is set
+  const float* oscale;  // [n][c_p] or null
+  const float* bias;    // [c_p] or null: x = conv * oscale + bias (for the ydot partials)
+  float* ydot;          // [n][tiles][c_p] per-tile sum of gx * (x - bias), or null
+  int out_bf16;
   int c_p;
   int in_h, in_w, out_h, out_w;
   int p0;            // leading padding (px0 == py0)
@@ -95,7 +99,6 @@ __global__ void __launch_bounds__(NT) flrelu_bwd_kernel(FlrBwdArgs a) {
   const int c0 = cb * 2 * NP;
   const TI* __restrict__ xin = reinterpret_cast<const TI*>(a.x) + (int64_t)n * a.in_h * a.in_w * a.c_p;
   const TG* __restrict__ gin = reinterpret_cast<const TG*>(a.gout) + (int64_t)n * a.out_h * a.out_w * a.c_p;
-  float* __restrict__ gx = a.gx + (int64_t)n * a.in_h * a.in_w * a.c_p;
 
   // ---------------- stage A: vertical passes
   for (int item = threadIdx.x; item < (NJX + NOX) * NP; item += NT) {
@@ -194,35 +197,70 @@ __global__ void __launch_bounds__(NT) flrelu_bwd_kernel(FlrBwdArgs a) {
   __syncthreads();
 
   // ---------------- stage C: vertical down-by-up pass per column, store
+  // Optional epilogue (the modulated conv's backward, x = conv * oscale + bias): gx * oscale is stored (bf16 for
+  // the dgrad GEMM), and sum gx * (x - bias) over the tile goes to ydot -> d oscale = sum / oscale on the host.
   constexpr int S3 = (TIY % 2 == 0 && TIX * NP * 2 <= NT) ? 2 : 1;
   constexpr int RG = TIY / S3;
   constexpr int RGK = (RG - 1) * UP + TU;
-  for (int item = threadIdx.x; item < TIX * NP * S3; item += NT) {
-    const int p = item % NP;
+  constexpr int NITEM = TIX * NP * S3;
+  static_assert(NITEM <= NT, "stage C: one item per thread");
+  bf2v ydp = bf2v{0.f, 0.f};
+  const int item = threadIdx.x;
+  const int p = item % NP;
+  const int c = c0 + 2 * p;
+  if (item < NITEM) {
     const int ix = (item / NP) % TIX;
     const int rg = item / (NP * TIX);
     const int gxx = i0x + ix;
-    if (gxx >= a.in_w) continue;
-    const int c = c0 + 2 * p;
-    bf2v o[RG];
+    if (gxx < a.in_w) {
+      bf2v o[RG];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) o[r] = bf2v{0.f, 0.f};
-    const int kb = rg * RG * UP;
+      for (int r = 0; r < RG; ++r) o[r] = bf2v{0.f, 0.f};
+      const int kb = rg * RG * UP;
 #pragma unroll
-    for (int kk = 0; kk < RGK; ++kk) {
-      const bf2v v = a_v[((kb + kk) * PA + ix) * NP + p];
+      for (int kk = 0; kk < RGK; ++kk) {
+        const bf2v v = a_v[((kb + kk) * PA + ix) * NP + p];
 #pragma unroll
-      for (int m = 0; m < TU / UP; ++m) {
-        const int r = (kk - TU + UP + UP * TU) / UP - TU + m;
-        const int t = r * UP + TU - 1 - kk;
-        if (r >= 0 && r < RG && t >= 0 && t < TU) o[r] += a.gu[t] * v;
+        for (int m = 0; m < TU / UP; ++m) {
+          const int r = (kk - TU + UP + UP * TU) / UP - TU + m;
+          const int t = r * UP + TU - 1 - kk;
+          if (r >= 0 && r < RG && t >= 0 && t < TU) o[r] += a.gu[t] * v;
+        }
+      }
+      bf2v os = bf2v{1.f, 1.f}, bi = bf2v{0.f, 0.f};
+      if (a.oscale) os = bf2v{a.oscale[(int64_t)n * a.c_p + c], a.oscale[(int64_t)n * a.c_p + c + 1]};
+      if (a.bias) bi = bf2v{a.bias[c], a.bias[c + 1]};
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const int gyy = i0y + rg * RG + r;
+        if (gyy >= a.in_h) continue;
+        const int64_t e = ((int64_t)gyy * a.in_w + gxx) * a.c_p + c;
+        if (a.ydot) {
+          const bf2v xv = ldp<TI>(xin + e, true);
+          ydp += o[r] * (xv - bi);
+        }
+        const bf2v v = o[r] * os;
+        if (a.out_bf16) {
+          bf16_t* po = reinterpret_cast<bf16_t*>(a.gx) + (int64_t)n * a.in_h * a.in_w * a.c_p + e;
+          *reinterpret_cast<uint32_t*>(po) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+        } else {
+          float* po = reinterpret_cast<float*>(a.gx) + (int64_t)n * a.in_h * a.in_w * a.c_p + e;
+          *reinterpret_cast<float2*>(po) = make_float2(v.x, v.y);
+        }
       }
     }
-    float* po = gx + (int64_t)gxx * a.c_p + c;
-#pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      const int gyy = i0y + rg * RG + r;
-      if (gyy < a.in_h) *reinterpret_cast<float2*>(po + (int64_t)gyy * a.in_w * a.c_p) = make_float2(o[r].x, o[r].y);
+  }
+  if (a.ydot) {  // fixed-order reduction of the tile's items per channel pair (LDS reused after a barrier)
+    __syncthreads();
+    if (item < NITEM) a_v[item] = ydp;
+    __syncthreads();
+    if (item < NP) {
+      bf2v t = bf2v{0.f, 0.f};
+      for (int k = item; k < NITEM; k += NP) t += a_v[k];
+      const int tile = ty * a.tiles_x + tx;
+      float* py = a.ydot + ((int64_t)n * a.tiles_y * a.tiles_x + tile) * a.c_p + c;
+      py[0] = t.x;
+      py[1] = t.y;
     }
   }
 }
@@ -242,10 +280,18 @@ static void fb_launch(const FlrBwdArgs& a, int ti, int tg, int grid, hipStream_t
 
 using namespace ic2;
 
-extern "C" int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout, int g_dtype, float* gx, int n, int c_p,
-                                   int in_h, int in_w, int out_h, int out_w, const float* fu, int fu_taps,
-                                   const float* fd, int fd_taps, int up, int down, int px0, int px1, int py0, int py1,
-                                   float gain, float slope, float clamp, int flip, void* stream) {
+extern "C" int64_t ic2_flrelu_bwd_ydot_floats(int n, int c_p, int in_h, int in_w, int up) {
+  const int tiy = 16, tix = 16;  // the default tile variant
+  (void)up;
+  return (int64_t)n * ceil_div(in_h, tiy) * ceil_div(in_w, tix) * c_p;
+}
+
+extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* gout, int g_dtype, void* gx,
+                                      int gx_dtype, int n, int c_p, int in_h, int in_w, int out_h, int out_w,
+                                      const float* fu, int fu_taps, const float* fd, int fd_taps, int up, int down,
+                                      int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
+                                      int flip, const float* oscale, const float* bias, float* ydot,
+                                      int64_t ydot_floats, void* stream) {
   IC2_CHECK_ARG(x && gout && gx && fu && fd, "flrelu_bwd_nhwc: null pointer");
   IC2_CHECK_ARG(n > 0 && c_p > 0 && in_h > 0 && in_w > 0, "flrelu_bwd_nhwc: bad geometry");
   IC2_CHECK_ARG(x_dtype == IC2_F32 || x_dtype == IC2_F16, "flrelu_bwd_nhwc: x must be f32 or f16");
@@ -263,8 +309,10 @@ extern "C" int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout,
               up, down, fu_taps, fd_taps);
     return IC2_E_UNSUPPORTED;
   }
+  IC2_CHECK_ARG(gx_dtype == IC2_F32 || gx_dtype == IC2_BF16, "flrelu_bwd_nhwc: gx must be f32 or bf16");
   FlrBwdArgs a;
   a.x = x; a.gout = gout; a.gx = gx;
+  a.oscale = oscale; a.bias = bias; a.ydot = ydot; a.out_bf16 = gx_dtype == IC2_BF16;
   a.c_p = c_p; a.in_h = in_h; a.in_w = in_w; a.out_h = out_h; a.out_w = out_w; a.p0 = px0;
   a.slope = slope; a.gain = gain; a.lim = clamp >= 0.f ? clamp / gain : INFINITY;
   for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
@@ -291,6 +339,9 @@ extern "C" int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout,
   a.cblocks = c_p / (2 * np);
   const int64_t grid = (int64_t)n * a.tiles_y * a.tiles_x * a.cblocks;
   IC2_CHECK_ARG(grid < (1LL << 31), "flrelu_bwd_nhwc: grid too large");
+  IC2_CHECK_ARG(ydot == nullptr || (v == 1 && ydot_floats >= (int64_t)n * a.tiles_y * a.tiles_x * c_p),
+                "flrelu_bwd_nhwc: ydot needs the default tiles and %lld floats",
+                (long long)((int64_t)n * a.tiles_y * a.tiles_x * c_p));
   hipStream_t s = as_stream(stream);
 #define IC2_FB_R(U_, TU_, TIY_, TIX_, NP_, NT_)                                                     \
   do {                                                                                              \
@@ -309,4 +360,14 @@ extern "C" int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout,
 #undef IC2_FB_R
   IC2_CHECK_LAUNCH("flrelu_bwd_nhwc");
   return IC2_OK;
+}
+
+
+extern "C" int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout, int g_dtype, float* gx, int n, int c_p,
+                                   int in_h, int in_w, int out_h, int out_w, const float* fu, int fu_taps,
+                                   const float* fd, int fd_taps, int up, int down, int px0, int px1, int py0, int py1,
+                                   float gain, float slope, float clamp, int flip, void* stream) {
+  return ic2_flrelu_bwd_nhwc_ex(x, x_dtype, gout, g_dtype, gx, IC2_F32, n, c_p, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
+                                fd_taps, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, nullptr, nullptr,
+                                nullptr, 0, stream);
 }

@@ -47,6 +47,10 @@ struct IgemmArgs {
   int act;
   float slope, act_gain, clamp, out_mul;
   int out_layout, out_dtype;
+  // fused GroupNorm statistics (hconv only; ic2_conv3x3_gn_fwd): per (image, group, tile) f64 (sum, sumsq) of
+  // the stored (rounded) outputs of channels < gn_c; null = off
+  double* gn_part;
+  int gn_groups, gn_c;
 };
 
 template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
@@ -944,8 +948,9 @@ struct HcCfg {
   static constexpr int PER_T = (NPIECE + 511) / 512;
 };
 
-template <int CINP, int COUTP, int TH>
-__global__ void __launch_bounds__(512) hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
+template <int CINP, int COUTP, int TH, bool GN>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(CINP == 32 ? 4 : 1)))
+hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
   using C = HcCfg<CINP, COUTP, TH>;
   __shared__ __attribute__((aligned(16))) char lds[C::HALO_B + C::W_B];
   char* const halo = lds;
@@ -1031,6 +1036,16 @@ __global__ void __launch_bounds__(512) hconv_kernel(IgemmArgs a, int tiles_x, in
     const int t2 = t / tiles_x;
     const int ty = t2 % tiles_y;
     const int nn = t2 / tiles_y;
+    // GN (fused statistics, groups = 32 over all COUTP channels): CPG = COUTP / 32 channels per group, so a
+    // lane's 4 channels 16i + 4fh .. +3 fall in 4 / CPG groups
+    constexpr int CPG = COUTP / 32, GL = 4 / CPG;
+    float gs[C::OB][GL], gq[C::OB][GL];
+    if constexpr (GN) {
+#pragma unroll
+      for (int i = 0; i < C::OB; ++i)
+#pragma unroll
+        for (int r = 0; r < GL; ++r) gs[i][r] = gq[i][r] = 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < C::JB; ++j) {
       const int pb = wave + 8 * j;
@@ -1042,12 +1057,60 @@ __global__ void __launch_bounds__(512) hconv_kernel(IgemmArgs a, int tiles_x, in
       for (int i = 0; i < C::OB; ++i) {
         const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         ig_store4(a, p, nn, pix, 16 * i + 4 * fh, v);
+        if constexpr (GN) {  // statistics of the value as stored: bias added, rounded to bf16
+          const float4 bi = *reinterpret_cast<const float4*>(a.bias + 16 * i + 4 * fh);
+          const float bv[4] = {bi.x, bi.y, bi.z, bi.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float st = bf2f(f2bf(v[r] + bv[r]));
+            gs[i][r / CPG] += st;
+            gq[i][r / CPG] += st * st;
+          }
+        }
       }
+    }
+    if constexpr (GN) {
+      // wave: sum over the 16 pixel lanes; workgroup: 8 waves through LDS (the halo region, after a barrier);
+      // then one thread per group sums the waves in a fixed order -> part[(nn, g, tile)]
+#pragma unroll
+      for (int i = 0; i < C::OB; ++i)
+#pragma unroll
+        for (int r = 0; r < GL; ++r)
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) {
+            gs[i][r] += __shfl_xor(gs[i][r], off, 64);
+            gq[i][r] += __shfl_xor(gq[i][r], off, 64);
+          }
+      __syncthreads();  // every wave is past its halo reads
+      float* red = reinterpret_cast<float*>(halo);  // [2][8 waves][32 groups]
+      if (fr == 0) {
+#pragma unroll
+        for (int i = 0; i < C::OB; ++i)
+#pragma unroll
+          for (int r = 0; r < GL; ++r) {
+            const int g = (16 * i + 4 * fh) / CPG + r;
+            red[wave * 32 + g] = gs[i][r];
+            red[(8 + wave) * 32 + g] = gq[i][r];
+          }
+      }
+      __syncthreads();
+      if (tid < 32) {
+        double sg = 0.0, qg = 0.0;
+#pragma unroll
+        for (int w8 = 0; w8 < 8; ++w8) {
+          sg += (double)red[w8 * 32 + tid];
+          qg += (double)red[(8 + w8) * 32 + tid];
+        }
+        double* o = a.gn_part + (((int64_t)nn * 32 + tid) * (tiles_x * tiles_y) + (ty * tiles_x + tx)) * 2;
+        o[0] = sg;
+        o[1] = qg;
+      }
+      // the next tile's first barrier orders these LDS reads before its halo stores
     }
   }
 }
 
-template <int CINP, int COUTP>
+template <int CINP, int COUTP, bool GN = false>
 static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
   constexpr int TH = CINP > 64 ? 4 : 8;  // 96 channels: 4-row tiles keep halo + weight within 160 KB of LDS
   const int tiles_x = (int)ceil_div(a.wo, 32), tiles_y = (int)ceil_div(a.ho, TH);
@@ -1057,11 +1120,11 @@ static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hconv_kernel<CINP, COUTP, TH>, 512, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hconv_kernel<CINP, COUTP, TH, GN>, 512, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((hconv_kernel<CINP, COUTP, TH>), dim3((unsigned)grid), dim3(512), 0, s, a, tiles_x, tiles_y,
+  hipLaunchKernelGGL((hconv_kernel<CINP, COUTP, TH, GN>), dim3((unsigned)grid), dim3(512), 0, s, a, tiles_x, tiles_y,
                      ntiles);
 }
 
@@ -1186,6 +1249,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
   a.out_layout = out_layout; a.out_dtype = out_dtype;
+  a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
   static const int group = [] {
     const char* e = getenv("IC2_IGEMM_GROUP");
     const int g = e ? atoi(e) : 1;  // 1 = o-tiles of a p-tile side by side (measured best)
@@ -1231,6 +1295,61 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   IC2_CHECK_LAUNCH("conv_igemm");
   return IC2_OK;
 }
+
+namespace ic2 {
+// conv (bias only, NHWC bf16 out) with the GroupNorm partial sums fused into the halo conv's epilogue when that
+// kernel is the one the dispatcher picks.  Returns the number of per-image chunks written to `part`
+// ([n][groups][chunks][2] f64), 0 when the conv ran unfused (the caller then computes the statistics itself),
+// or -1 on an argument error (message set).
+int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
+                  int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
+                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  const int64_t M = (int64_t)n * ho * wo;
+  const bool hconv = hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
+  const int th = cin_p > 64 ? 4 : 8;
+  const int64_t nch = ceil_div(wo, 32) * ceil_div(ho, th);
+  // fused instances: 32 groups over all cout_p channels (VGGBlock: GroupNorm(min(32, c), c) with c = 32 / 64).
+  // Off by default: measured on MI355X the epilogue reduction (two extra barriers per tile in the persistent
+  // kernel) costs what the saved read of y gains -- C4 357.1 -> 356.7 img/s, C2 1277 -> 1256 (profiles/
+  // r2b_conv_gn_ab.txt); IC2_CONV_GN=1 enables it.
+  static const bool fuse_env = [] {
+    const char* e = getenv("IC2_CONV_GN");
+    return e && e[0] == '1';
+  }();
+  const bool fuse = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
+  if (!fuse || !hconv || part == nullptr || part_doubles < (int64_t)n * groups * nch * 2 || groups != 32 ||
+      cout_valid != cout_p || bias == nullptr) {
+    const int rc = ic2_conv_igemm_ws(x, w, y, dtype, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo,
+                                     nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace, ws_bytes, s);
+    return rc == IC2_OK ? 0 : -1;
+  }
+  IgemmArgs a;
+  a.x = x; a.w = w; a.y = y; a.oscale = nullptr; a.bias = bias; a.ws = nullptr;
+  a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
+  a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
+  a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
+  a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = 1.f;
+  a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = dtype;
+  a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
+  a.group = 1;
+  if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);
+  else if (cin_p == 32) launch_hconv<32, 64, true>(a, s);
+  else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32, true>(a, s);
+  else if (cin_p == 64) launch_hconv<64, 64, true>(a, s);
+  else if (cout_p == 32) launch_hconv<96, 32, true>(a, s);
+  else launch_hconv<96, 64, true>(a, s);
+  return (int)nch;
+}
+
+int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
+                                   int groups) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (!hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw)) return 0;
+  const int th = cin_p > 64 ? 4 : 8;
+  return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, th) * 2;
+}
+}  // namespace ic2
 
 extern "C" int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
                               int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,

@@ -411,17 +411,17 @@ class SynthesisLayer(torch.nn.Module):
         """Autograd step: x NHWC [n, in, in, cin_p] (dt, NOT yet scaled by xscale), w [n, w_dim] f32 ->
         NHWC [n, out, out, cout_p] dt, or for ToRGB the NCHW f32 image * final_scale."""
         xs, os_ = self.modulation_train(w)
+        if not self.is_torgb:
+            return ao.SynthLayerNHWC.apply(x.contiguous(), xs.contiguous(), os_.contiguous(), self, dt)
+        # ToRGB (1x1, 3 channels, linear + clamp): frozen conv on MFMA, the rest as torch ops
         a = x * xs[:, None, None, :].to(x.dtype)
-        k = self.conv_kernel
         wp, _, bp = self.packed(dt)
-        c = ao.FrozenConvNHWC.apply(a, wp, self.packed_adjoint(dt), k, k - 1, self.out_channels, self.in_channels)
+        c = ao.FrozenConvNHWC.apply(a, wp, self.packed_adjoint(dt), 1, 0, self.out_channels, self.in_channels)
         y = c * os_[:, None, None, :] + bp
-        if self.is_torgb:
-            if self.conv_clamp is not None:
-                y = y.clamp(-float(self.conv_clamp), float(self.conv_clamp))
-            img = y[..., : self.out_channels].permute(0, 3, 1, 2)
-            return img if final_scale is None else img * float(final_scale)
-        return ao.FilteredLReluNHWC.apply(y, self, dt)
+        if self.conv_clamp is not None:
+            y = y.clamp(-float(self.conv_clamp), float(self.conv_clamp))
+        img = y[..., : self.out_channels].permute(0, 3, 1, 2)
+        return img if final_scale is None else img * float(final_scale)
 
     def forward(self, x, w, noise_mode="random", force_fp32=False, update_emas=False):
         """Layer-level API (NCHW f32 in/out), as SG3's SynthesisLayer.forward."""

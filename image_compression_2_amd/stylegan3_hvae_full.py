@@ -41,8 +41,7 @@ class _Act:
         self.c = c
 
 
-def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
-    """nn.Conv2d (3x3 or k x k, stride 1, 'same' padding) + bias on MFMA."""
+def _packed(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     cout, cin, kh, kw = conv.weight.shape
     assert conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and cin == x.c
     pad = conv.padding[0]
@@ -59,7 +58,14 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
             bp[:cout] = conv.bias.detach().float()
         hit = (key, (wp, bp))
         cache[id(conv)] = hit
-    wp, bp = hit[1]
+    return hit[1]
+
+
+def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
+    """nn.Conv2d (3x3 or k x k, stride 1, 'same' padding) + bias on MFMA."""
+    cout, cin, kh, kw = conv.weight.shape
+    pad = conv.padding[0]
+    wp, bp = _packed(conv, x, dt, cache, stream)
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
     y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
@@ -69,13 +75,33 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     return _Act(y, cout)
 
 
-def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2):
-    """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2))."""
+def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stream, fuse=-1):
+    """conv (+ bias) and the GroupNorm statistics of its output in one call (ic2_conv3x3_gn_fwd: fused into the
+    halo conv's epilogue where that kernel runs the layer).  -> (y, stats)."""
+    cout, cin, kh, kw = conv.weight.shape
+    pad = conv.padding[0]
+    wp, bp = _packed(conv, x, dt, cache, stream)
+    cout_p = wp.shape[0]
+    ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
+    dc = nv.dtype_code(dt)
+    y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
+    nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad, norm.num_groups))
+    stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
+    nbytes = int(nv.query("ic2_conv_igemm_ws_bytes", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad))
+    ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=x.t.device) if nbytes > 0 else None
+    nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), dc, x.n, x.h, x.w, x.c_p, cout_p, cout, kh, kw,
+            pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, nv.ptr(ws), nbytes, int(fuse), stream)
+    return _Act(y, cout), stats
+
+
+def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None):
+    """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2)); `stats` from _conv_gn, else computed here."""
     groups = norm.num_groups
-    nfl = int(nv.query("ic2_group_norm_stats_floats", y.n, y.h * y.w, groups))
-    stats = torch.empty([nfl], dtype=torch.float32, device=y.t.device)
-    nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
-            float(norm.eps), nv.ptr(stats), stream)
+    if stats is None:
+        nfl = int(nv.query("ic2_group_norm_stats_floats", y.n, y.h * y.w, groups))
+        stats = torch.empty([nfl], dtype=torch.float32, device=y.t.device)
+        nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
+                float(norm.eps), nv.ptr(stats), stream)
     oh, ow = (y.h // 2, y.w // 2) if pool else (y.h, y.w)
     out = torch.empty([y.n, oh, ow, y.c_p], dtype=dt, device=y.t.device)
     nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype), nv.dtype_code(dt), y.n, y.h, y.w,
@@ -238,11 +264,11 @@ class VGGBlock(nn.Module):
         self._cache = {}
 
     def run_nhwc(self, x: _Act, dt, cache, stream):
-        y = _conv(self.conv1, x, dt, cache, stream)
-        h = _group_norm_lrelu(self.norm1, y, False, dt, stream)
-        y = _conv(self.conv2, h, dt, cache, stream)
+        y, st = _conv_gn(self.conv1, self.norm1, x, dt, cache, stream)
+        h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st)
+        y, st = _conv_gn(self.conv2, self.norm2, h, dt, cache, stream)
         pool = y.h > 1 and y.w > 1
-        return _group_norm_lrelu(self.norm2, y, pool, dt, stream)
+        return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st)
 
     def forward_train_nhwc(self, h, dt):
         """Autograd path of run_nhwc: (NHWC activation, valid channels) -> the same after the block."""

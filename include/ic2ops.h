@@ -235,6 +235,21 @@ int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y
 /* Backward of ic2_global_avg_pool (AdaptiveAvgPool2d(1), :218): dx [n][hw][c_p] = dpooled [n][c] / hw. */
 int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_p, int c, void* stream);
 
+/* VGGBlock conv + GroupNorm statistics (SURVEY 8b `ic2_conv3x3_gn_fwd`; stylegan3_hvae_full.py:175-191, the
+ * conv1/conv2 -> norm1/norm2 pairs): y = conv(x, w) + bias (NHWC, dtype = the activation dtype) and the GroupNorm
+ * (mean, rstd) per (sample, group) of y's first cout_valid channels in stats[0 .. 2*n*groups).  When the halo conv
+ * kernel runs the layer (bf16, cin_p <= 96, cout_p <= 64) the per-tile sums come out of its epilogue, computed on the
+ * stored (rounded) values, so y is not read a second time; otherwise the two-stage statistics pass of
+ * ic2_group_norm_stats runs after the conv.  stats: ic2_conv3x3_gn_stats_floats() floats (statistics + partial
+ * sums); conv_ws / conv_ws_bytes: the conv's split-K workspace as for ic2_conv_igemm_ws.  fuse: 1 = fused statistics
+ * where the halo conv runs, 0 = always the separate pass, -1 = default (separate; env IC2_CONV_GN=1 fuses -- measured
+ * at parity on MI355X).  Deterministic. */
+int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad,
+                                    int groups);
+int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
+                       int cout_valid, int kh, int kw, int pad, const float* bias, int groups, float eps, float* stats,
+                       int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse, void* stream);
+
 /* Backward of ic2_flrelu_nhwc w.r.t. its input (SynthesisLayer's filtered_lrelu, SG3-public; the encoder's loss
  * reaches W+ through it, :669-696): x = the forward's input (NHWC [n][in_h][in_w][c_p], f32 or f16), gout = the
  * gradient of its output (NHWC [n][out_h][out_w][c_p], f32 or bf16) -> gx (NHWC, f32).  Recomputes the upsampled
@@ -245,6 +260,24 @@ int ic2_flrelu_bwd_nhwc(const void* x, int x_dtype, const void* gout, int g_dtyp
                         int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps,
                         int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
                         int flip, void* stream);
+
+/* ic2_flrelu_bwd_nhwc with the modulated conv's backward fused into its store (x = conv * oscale + bias, the
+ * synthesis conv epilogue): gx = (dL/dx) * oscale[n][c] (the gradient w.r.t. the raw conv output, f32 or bf16 for
+ * the dgrad GEMM), and ydot[n][tile][c] = per-tile sums of (dL/dx) * (x - bias[c]) -> dL/doscale = sum / oscale.
+ * oscale / bias / ydot nullable.  ydot: ic2_flrelu_bwd_ydot_floats() floats. */
+int64_t ic2_flrelu_bwd_ydot_floats(int n, int c_p, int in_h, int in_w, int up);
+int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* gout, int g_dtype, void* gx, int gx_dtype, int n,
+                           int c_p, int in_h, int in_w, int out_h, int out_w, const float* fu, int fu_taps,
+                           const float* fd, int fd_taps, int up, int down, int px0, int px1, int py0, int py1,
+                           float gain, float slope, float clamp, int flip, const float* oscale, const float* bias,
+                           float* ydot, int64_t ydot_floats, void* stream);
+
+/* Backward of the synthesis input modulation a = x * xscale[n][c] (SG3 modulated_conv2d's style multiply in the
+ * activation-scaling form): dx = da * xscale (NHWC, f32 / bf16) and part[n][chunk][c] = per-chunk sums of da * x
+ * (dL/dxscale = sum over chunks).  part: ic2_scale_bwd_part_floats() floats.  Deterministic. */
+int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p);
+int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw, int c_p,
+                       float* part, int64_t part_floats, void* stream);
 
 #ifdef __cplusplus
 }

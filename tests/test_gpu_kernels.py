@@ -409,6 +409,36 @@ def test_group_norm_lrelu_pool_matches_torch(cuda, n, c, groups, h, w, pool, dty
     assert _maxdiff(y, r) < tol * (1 + r.abs().max().item())
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w", [(32, 64, 2, 200, 181), (64, 64, 1, 257, 263), (3, 32, 2, 190, 200),
+                                             (64, 32, 2, 181, 190), (96, 64, 1, 300, 230), (128, 128, 2, 64, 70),
+                                             (32, 64, 1, 16, 20)])
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_conv3x3_gn_fwd_statistics(cuda, cin, cout, n, h, w, fuse):
+    """ic2_conv3x3_gn_fwd: the conv output is the plain conv's, and the GroupNorm statistics -- fused
+    into the halo conv's epilogue for the bf16 <= 96 -> <= 64 channel layers (edge tiles included), the separate
+    pass otherwise -- match ic2_group_norm_stats on the same stored output (fp64 partial sums, 1e-5 relative)."""
+    from image_compression_2_amd.stylegan3_hvae_full import _conv_gn
+    g = torch.Generator().manual_seed(cin + cout + h)
+    x = torch.randn(n, cin, h, w, generator=g)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1).to(cuda)
+    norm = torch.nn.GroupNorm(min(32, cout), cout).to(cuda)
+    stream = nv.stream_of()
+    xin = _to_nhwc(x.to(cuda), torch.bfloat16, stream)
+    y_ref = _conv(conv, xin, torch.bfloat16, {}, stream)
+    y, st = _conv_gn(conv, norm, xin, torch.bfloat16, {}, stream, fuse=fuse)
+    assert torch.equal(y.t, y_ref.t)
+    groups = norm.num_groups
+    nfl = int(nv.query("ic2_group_norm_stats_floats", n, h * w, groups))
+    ref = torch.empty([nfl], dtype=torch.float32, device=cuda)
+    nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.BF16, n, h * w, y.c_p, cout, groups, float(norm.eps), nv.ptr(ref),
+            stream)
+    a, b = st[: n * groups * 2].view(-1, 2).cpu(), ref[: n * groups * 2].view(-1, 2).cpu()
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
+    # and against torch on the same rounded tensor
+    yt = y.t.float()[..., :cout].permute(0, 3, 1, 2).reshape(n, groups, -1).double()
+    assert torch.allclose(a[:, 0].double(), yt.mean(-1).reshape(-1).cpu(), rtol=1e-5, atol=1e-6)
+
+
 # ------------------------------------------------------------------ metric / resize
 @pytest.mark.parametrize("shape", [(3, 3, 16, 16), (2, 3, 7, 5), (1, 3, 256, 256)])
 def test_uint8_sse_matches_reference_definition(cuda, shape):

@@ -397,3 +397,25 @@ def test_flrelu_backward_kernel(cuda, gen256_frozen, li, mode):
     e = _rel(got[..., :c].permute(0, 3, 1, 2), yr.grad)
     print(f"[flrelu-bwd L{li} {mode}] rel err {e:.2e}")
     assert e < 1e-3
+
+
+@pytest.mark.parametrize("cp,hw,n", [(512, 38 * 38, 2), (192, 278 * 277, 1), (64, 1000, 3)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_scale_backward_kernel(cuda, cp, hw, n, dtype):
+    """ic2_scale_bwd_nhwc: dx = da * xscale and d xscale = sum_p da * x (per-chunk partials summed on the host)."""
+    g = torch.Generator().manual_seed(cp)
+    da = torch.randn(n, hw, cp, generator=g).to(dtype)
+    x = torch.randn(n, hw, cp, generator=g).to(dtype)
+    xs = torch.randn(n, cp, generator=g)
+    dad, xd, xsd = da.to(cuda), x.to(cuda), xs.to(cuda)
+    dx = torch.empty_like(xd)
+    npart = int(nv.query("ic2_scale_bwd_part_floats", n, hw, cp))
+    part = torch.empty([npart], dtype=torch.float32, device=cuda)
+    nv.call("ic2_scale_bwd_nhwc", nv.ptr(dad), nv.ptr(xd), nv.ptr(xsd), nv.ptr(dx), nv.dtype_code(dtype), n, hw, cp,
+            nv.ptr(part), npart, nv.stream_of())
+    ref_dx = (da.double() * xs.double()[:, None, :]).to(dtype)
+    assert torch.equal(dx.cpu(), ref_dx) if dtype == torch.float32 else (dx.cpu().float() - ref_dx.float()).abs().max() \
+        <= 2 ** -7 * ref_dx.float().abs().max()
+    dxs = part.view(n, -1, cp).sum(1).cpu().double()
+    ref = (da.double() * x.double()).sum(1)
+    assert _rel(dxs, ref) < 1e-5
