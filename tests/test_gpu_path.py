@@ -308,16 +308,22 @@ def test_codebook_container_round_trip(cuda, gen256, tmp_path, golden_dir):
 
 
 def test_forwards_refuse_autograd_on_gpu(cuda, gen256):
-    """With grad enabled and parameters requiring grad the HIP forwards raise instead of returning tensors
-    with no graph (a reference training loop would otherwise run and learn nothing)."""
+    """With grad enabled the forwards either build a graph through the HIP backward kernels (encoder; synthesis
+    w.r.t. ws with G frozen) or raise (gradients w.r.t. G's weights) -- never a silent graph-less result."""
     with torch.enable_grad():
         enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32).to(cuda)
         x = torch.rand(1, 3, 32, 32, device=cuda)
         w, m, lv = enc(x)  # the encoder has a HIP autograd path (test_gpu_training.py)
         assert m.grad_fn is not None
-        ws = torch.zeros(1, 16, 512, device=cuda, requires_grad=True)
-        with pytest.raises(nv.AutogradUnsupported):
-            gen256.synthesis(ws)
+        ws = torch.randn(1, 16, 512, device=cuda, requires_grad=True)
+        gen256.requires_grad_(True)
+        try:
+            with pytest.raises(nv.AutogradUnsupported):
+                gen256.synthesis(ws)           # gradients w.r.t. G's weights are not implemented
+        finally:
+            gen256.requires_grad_(False)
+        img = gen256.synthesis(ws)             # frozen G (as the reference trains): the HIP autograd path
+        assert img.grad_fn is not None
         # compress is an inference API with a rounded output: it runs
         comp = ic2.StyleGAN3Compressor(enc, gen256)
         assert comp.compress(x).shape == (1, 16, 512)
