@@ -455,7 +455,7 @@ def run(args):
                            "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}
     elif not dry and not args.no_roofline:
         conv_names = ("ic2_conv_igemm", "ic2_conv_igemm_ws")
-        timer = CallTimer(nv, conv_names + ("ic2_flrelu_nhwc",))
+        timer = CallTimer(nv, conv_names + ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16"))
         timer.install()
         timer.enabled = True
         n_inst = min(args.steps, 10)
@@ -463,7 +463,7 @@ def run(args):
         timer.enabled = False
         timer.uninstall()
         conv_ms, n_launch = timer.total(conv_names)
-        flr_ms, n_flr = timer.total(("ic2_flrelu_nhwc",))
+        flr_ms, n_flr = timer.total(("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16"))
         flops_img = algorithmic_flops_per_image(enc, G, res)
         peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
         traffic, traffic_src = pmc_traffic(args.config, args.precision, batch)

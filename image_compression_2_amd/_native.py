@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libic2ops.so")
 
 F32, BF16, F16 = 0, 1, 2
 ACT_LINEAR, ACT_LRELU = 0, 1
-NHWC, NCHW = 0, 1
+NHWC, NCHW, NHWC16 = 0, 1, 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -37,6 +37,8 @@ _SIGS = {
                            _F, _I, _P],
     "ic2_flrelu_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F,
                         _I, _P, _P],
+    "ic2_flrelu_nhwc16": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _F,
+                          _F, _I, _P, _P],
     "ic2_fc": [_P, _I64, _P, _P, _P, _I, _I, _I, _F, _F, _I, _F, _F, _P],
     "ic2_pack_weight": [_P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _I, _P, _P],
     "ic2_modconv_prep": [_P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P],

@@ -11,6 +11,7 @@ struct FlrArgs {
   const float* bias;
   const float* post_scale;  // [n][c_p] or null
   int64_t xsn, xsy, xsx, xsc;  // input strides (elements)
+  int64_t xcb;                 // MFMA kernels: offset of the next 16-channel block (16 NHWC, 16*h*w blocked)
   int64_t ysn, ysy, ysx, ysc;  // output strides
   int c, c_p;                   // valid channels, post_scale row stride
   int in_h, in_w, out_h, out_w;
@@ -22,7 +23,7 @@ struct FlrArgs {
   float gd[12];  // flipped (unless flip_filter)
 };
 
-// NHWC, f16 (in_f16) or bf16 input, bf16 output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
+// NHWC or channel-blocked NHWC16 (strides in a), f16 (in_f16) or bf16 input, bf16 output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
 // bias (folded into the producer).  Sets tiles/cblocks itself.  Returns IC2_E_UNSUPPORTED when the
 // configuration has no MFMA instance.
 int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, int delta, int n, hipStream_t s);

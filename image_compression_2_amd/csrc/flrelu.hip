@@ -307,7 +307,7 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
                          int in_h, int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd,
                          int fd_taps, const float* b, int up, int down, int px0, int px1, int py0, int py1,
                          float gain, float slope, float clamp, int flip, const float* post_scale, void* stream,
-                         const char* name) {
+                         const char* name, bool in_blocked = false) {
   IC2_CHECK_ARG(x && y, "%s: null pointer", name);
   IC2_CHECK_ARG(n > 0 && c > 0 && in_h > 0 && in_w > 0 && up >= 1 && down >= 1, "%s: bad geometry", name);
   IC2_CHECK_ARG(fu_taps >= 1 && fd_taps >= 1 && fu_taps <= 24 && fd_taps <= 12, "%s: unsupported taps", name);
@@ -328,7 +328,12 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   }
   FlrArgs a;
   a.x = x; a.y = y; a.bias = b; a.post_scale = post_scale;
-  if (chlast) {
+  a.xcb = 16;
+  if (in_blocked) {  // channel-blocked NHWC16 input: [n][c_p / 16][in_h][in_w][16]
+    a.xsc = 1; a.xsx = 16; a.xsy = (int64_t)in_w * 16; a.xsn = (int64_t)in_h * in_w * c_p;
+    a.xcb = (int64_t)in_h * in_w * 16;
+    a.ysc = 1; a.ysx = c_p; a.ysy = (int64_t)out_w * c_p; a.ysn = (int64_t)out_h * out_w * c_p;
+  } else if (chlast) {
     a.xsc = 1; a.xsx = c_p; a.xsy = (int64_t)in_w * c_p; a.xsn = (int64_t)in_h * in_w * c_p;
     a.ysc = 1; a.ysx = c_p; a.ysy = (int64_t)out_w * c_p; a.ysn = (int64_t)out_h * out_w * c_p;
   } else {
@@ -362,6 +367,11 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
       IC2_CHECK_LAUNCH(name);
       return IC2_OK;
     }
+  }
+  if (in_blocked) {
+    set_error("%s: channel-blocked input needs the MFMA instance (f16/bf16 in, bf16 out, no bias, up 2/4 with 6*up "
+              "taps, down 2 / 12 taps)", name);
+    return IC2_E_UNSUPPORTED;
   }
   if (dtype_in == IC2_F16) {
     set_error("%s: f16 input needs the MFMA instance (NHWC, bf16 out, no bias, up 2/4 with 6*up taps, down 2 / 12 taps)",
@@ -426,4 +436,16 @@ extern "C" int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_o
   return flrelu_common(x, y, dtype_in, dtype_out, true, n, c_p, c_p, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
                        fd_taps, b, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, post_scale, stream,
                        "flrelu_nhwc");
+}
+
+extern "C" int ic2_flrelu_nhwc16(const void* x, void* y, int dtype_in, int dtype_out, int n, int c_p, int in_h,
+                                 int in_w, int out_h, int out_w, const float* fu, int fu_taps, const float* fd,
+                                 int fd_taps, const float* b, int up, int down, int px0, int px1, int py0, int py1,
+                                 float gain, float slope, float clamp, int flip, const float* post_scale,
+                                 void* stream) {
+  IC2_CHECK_ARG(c_p % 16 == 0, "flrelu_nhwc16: c_p must be a multiple of 16");
+  IC2_CHECK_ARG(dtype_in == IC2_F16 || dtype_in == IC2_BF16, "flrelu_nhwc16: f16 or bf16 input");
+  return flrelu_common(x, y, dtype_in, dtype_out, true, n, c_p, c_p, in_h, in_w, out_h, out_w, fu, fu_taps, fd,
+                       fd_taps, b, up, down, px0, px1, py0, py1, gain, slope, clamp, flip, post_scale, stream,
+                       "flrelu_nhwc16", true);
 }

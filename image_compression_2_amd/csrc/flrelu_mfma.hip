@@ -220,12 +220,13 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
     dma_yx[i] = (k < NDMA && e < NCH) ? (jy | (x << 16)) : -1;
   }
   const int half8 = (lane & 1) * 8;
+  const int xsy = (int)a.xsy, xsx = (int)a.xsx;  // < 2^31: checked by the launcher (per-sample image < 2 GiB)
   auto chunk_src = [&](int e, int n, int sy0, int sx0, int c0) -> const void* {
     const int pix = e >> 1, half = e & 1;
     const int jy = pix / NIN, x = pix - jy * NIN;
     const int iy = sy0 + jy, ix = sx0 + x;
     const bool ok = e < NCH && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
-    const uint16_t* src = xin + (((int64_t)n * a.in_h + iy) * a.in_w + ix) * a.c_p + c0 + half * 8;
+    const uint16_t* src = xin + n * a.xsn + (c0 >> 4) * a.xcb + iy * a.xsy + ix * a.xsx + half * 8;
     return ok ? (const void*)src : zero_line();
   };
   auto load_tile = [&](int t) {
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
     const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
     if constexpr (IN_F16) {
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(xin + (int64_t)n * a.in_h * a.in_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
+          (void*)(xin + n * a.xsn + (c0 >> 4) * a.xcb), 0, FM_OOB, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NDW; ++i) {
         const int k = wave + NW * i;
@@ -242,7 +243,7 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
           const int yx = dma_yx[i];
           const int iy = sy0 + (yx & 0xffff), ix = sx0 + (yx >> 16);
           const bool ok = yx >= 0 && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
-          const uint32_t off = ok ? (uint32_t)(((iy * a.in_w + ix) * a.c_p + half8) * 2) : FM_OOB;
+          const uint32_t off = ok ? (uint32_t)((iy * xsy + ix * xsx + half8) * 2) : FM_OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(in_img + k * 256), 16,
                                                    off, 0, 0, 0);
         }
@@ -478,7 +479,7 @@ struct FmGeom2 {
   static_assert(NBX == 2 * NOB + 1, "horizontal down: output block ob reads grid blocks 2ob .. 2ob+2");
 };
 
-template <int U, int DELTA, int TOX, int NW, bool CL>
+template <int U, int DELTA, int TOX, int NW, bool CL, int ABL>
 __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs a, int ntiles) {  // 2 WGs / CU
   constexpr int NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;  // grid rows per wave per block; output columns per wave
   using G = FmGeom2<U, TOX>;
@@ -529,12 +530,13 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
     dma_yx[i] = (k < NDMA && e < NCH) ? (jy | (x << 16)) : -1;
   }
   const int half8 = (lane & 1) * 8;
+  const int xsy = (int)a.xsy, xsx = (int)a.xsx;  // < 2^31: checked by the launcher (per-sample image < 2 GiB)
   auto load_tile = [&](int t) {
     int n, oy0, ox0, c0;
     tile_geom(t, n, oy0, ox0, c0);
     const int sy0 = (oy0 * 2 - a.py0 + DELTA) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(xin + (int64_t)n * a.in_h * a.in_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
+        (void*)(xin + n * a.xsn + (c0 >> 4) * a.xcb), 0, FM_OOB, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NDW; ++i) {
       const int k = wave + NW * i;
@@ -542,7 +544,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
         const int yx = dma_yx[i];
         const int iy = sy0 + (yx & 0xffff), ix = sx0 + (yx >> 16);
         const bool ok = yx >= 0 && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
-        const uint32_t off = ok ? (uint32_t)(((iy * a.in_w + ix) * a.c_p + half8) * 2) : FM_OOB;
+        const uint32_t off = ok ? (uint32_t)((iy * xsy + ix * xsx + half8) * 2) : FM_OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(in_img + k * 256), 16,
                                                  off, 0, 0, 0);
       }
@@ -570,9 +572,10 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
     for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)] * inv_lim;
     gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
-  // horizontal down matrices over kx blocks (K = 32 per MFMA).  Plain: [b0; b1], [b2; 0].  CL: taps * lim,
-  // [b0; b1], [b2; -b0], [-b1; -b2] against (pos0, pos1), (pos2, neg0), (neg1, neg2)
-  fm_h8 gdh01, gdh2, gdh3;
+  // horizontal down matrices over kx blocks (K = 32 per MFMA).  Plain: [b0; b1], [b2; 0] against (u0, u1),
+  // (u2, 0).  CL: taps * lim, [bi; -bi] against the quad (pos_i, neg_i) of grid block i: each block's quad is
+  // one register tuple, shared as-is by the two output blocks that read it (no operand copies)
+  fm_h8 gdh01, gdh2, gdq[3];
   {
     const float sc = CL ? a.lim : 1.f;
     auto tap = [&](int blk, int j) { return taps[228 + 16 * blk + 4 * g + j - 2 * li] * sc; };
@@ -586,15 +589,18 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       v[j] = tap(2, j);
-      v[4 + j] = CL ? -tap(0, j) : 0.f;
+      v[4 + j] = 0.f;
     }
     gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = -tap(1, j);
-      v[4 + j] = -tap(2, j);
+    for (int bi = 0; bi < 3; ++bi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = tap(bi, j);
+        v[4 + j] = -tap(bi, j);
+      }
+      gdq[bi] = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
     }
-    gdh3 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
   }
   fm_h4 gdv[3];
 #pragma unroll
@@ -645,10 +651,11 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
           *reinterpret_cast<uint2*>(v_img + li * G::V_PITCH + x * 8 + 2 * g) = fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
         }
       }
-      __syncthreads();
-      if (b == 2 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);  // input image dead: prefetch
+      if constexpr (!(ABL & 1)) __syncthreads();
+      if (!(ABL & 4) && b == 2 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);  // input image dead: prefetch
       // ---- horizontal: up (NBX column blocks), activation, down (NOB output blocks), one grid row of this
       // wave at a time (bounded register pressure: 2 workgroups per CU need <= 128 VGPRs)
+      if constexpr (!(ABL & 16))
 #pragma unroll
       for (int rr = 0; rr < RR; ++rr) {
         const int row = wave + NW * rr;
@@ -665,27 +672,37 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
           u[tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[tt]),
                                                         fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        uint2 au[NBX], an[NBX];
-#pragma unroll
-        for (int tt = 0; tt < NBX; ++tt) {
-          const uint32_t h0 = fm_h2u(u[tt][0], u[tt][1]), h1 = fm_h2u(u[tt][2], u[tt][3]);
-          if constexpr (CL) fm_act_split(h0, h1, nslope2, au[tt], an[tt]);
-          else au[tt] = fm_act_h4(h0, h1, slope2, nlim2, lim2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
         fm_f4 d[NOB];
-#pragma unroll
-        for (int ob = 0; ob < NOB; ++ob)
-          d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob], au[2 * ob + 1]), gdh01,
-                                                         fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-        for (int ob = 0; ob < NOB; ++ob)
-          d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob + 2], CL ? an[2 * ob] : make_uint2(0u, 0u)),
-                                                         gdh2, d[ob], 0, 0, 0);
         if constexpr (CL) {
+          fm_h8 q[NBX];  // (pos, neg) of grid block tt as one tuple
+#pragma unroll
+          for (int tt = 0; tt < NBX; ++tt) {
+            uint2 p, m;
+            if constexpr (ABL & 2) { p = make_uint2(fm_h2u(u[tt][0], u[tt][1]), fm_h2u(u[tt][2], u[tt][3])); m = p; }
+            else fm_act_split(fm_h2u(u[tt][0], u[tt][1]), fm_h2u(u[tt][2], u[tt][3]), nslope2, p, m);
+            q[tt] = fm_h8_of(p, m);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int bi = 0; bi < 3; ++bi)
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob)
+              d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(q[2 * ob + bi], gdq[bi],
+                                                             bi == 0 ? fm_f4{0.f, 0.f, 0.f, 0.f} : d[ob], 0, 0, 0);
+        } else {
+          uint2 au[NBX];
+#pragma unroll
+          for (int tt = 0; tt < NBX; ++tt)
+            au[tt] = fm_act_h4(fm_h2u(u[tt][0], u[tt][1]), fm_h2u(u[tt][2], u[tt][3]), slope2, nlim2, lim2);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int ob = 0; ob < NOB; ++ob)
-            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(an[2 * ob + 1], an[2 * ob + 2]), gdh3, d[ob], 0, 0, 0);
+            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob], au[2 * ob + 1]), gdh01,
+                                                           fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob)
+            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob + 2], make_uint2(0u, 0u)), gdh2, d[ob],
+                                                           0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -693,17 +710,19 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
           *reinterpret_cast<uint2*>(d_img + row * G::D_PITCH + (16 * ob + li) * G::D_XP + 2 * g) =
               fm_pack4(d[ob][0], d[ob][1], d[ob][2], d[ob][3]);
       }
-      __syncthreads();
+      if constexpr (!(ABL & 1)) __syncthreads();
       // ---- vertical down: accumulate block b's 16 grid rows into this wave's output columns
-      fm_s4 da[OCW];
+      if constexpr (!(ABL & 32)) {
+        fm_s4 da[OCW];
 #pragma unroll
-      for (int i = 0; i < OCW; ++i)
-        da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + NW * i) * G::D_XP + 2 * tp);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < OCW; ++i)
+          da[i] = fm_tr_read(d_img + (4 * g + tq) * G::D_PITCH + (wave + NW * i) * G::D_XP + 2 * tp);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < OCW; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[b], acc[i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < OCW; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[b], acc[i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
 
     // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox)
@@ -725,7 +744,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   }
 }
 
-template <int U, int DELTA, bool CL>
+template <int U, int DELTA, bool CL, int ABL>
 static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
   constexpr int TOX = 32, NW = 8;
   a.tiles_x = (int)ceil_div(a.out_w, TOX);
@@ -737,11 +756,11 @@ static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL>, 64 * NW, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL, ABL>, 64 * NW, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, ntiles);
+  hipLaunchKernelGGL((flrelu_mfma2_kernel<U, DELTA, TOX, NW, CL, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, ntiles);
 }
 
 // the clamp-split activation needs a finite clamp whose reciprocal scaling keeps the f16 operands normal
@@ -752,8 +771,28 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
     const char* e = getenv("IC2_FLR_CLSPLIT");
     return !(e && e[0] == '0');
   }();
-  if (split && a.lim >= 0.0625f && a.lim <= 4096.f) fm2_launch_cl<U, DELTA, true>(a, n, s);
-  else fm2_launch_cl<U, DELTA, false>(a, n, s);
+  // IC2_FLR_ABL (diagnostic, gives WRONG results): bit 1 drops the in-tile barriers, 2 the activation VALU, 4 the
+  // input DMA, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
+  static const int abl = [] {
+    const char* e = getenv("IC2_FLR_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  if (split && a.lim >= 0.0625f && a.lim <= 4096.f) {
+    if constexpr ((U == 2 && DELTA == 1) || (U == 4 && DELTA == 2)) {
+      switch (abl) {
+        case 1: fm2_launch_cl<U, DELTA, true, 1>(a, n, s); return;
+        case 2: fm2_launch_cl<U, DELTA, true, 2>(a, n, s); return;
+        case 4: fm2_launch_cl<U, DELTA, true, 4>(a, n, s); return;
+        case 16: fm2_launch_cl<U, DELTA, true, 16>(a, n, s); return;
+        case 32: fm2_launch_cl<U, DELTA, true, 32>(a, n, s); return;
+        case 7: fm2_launch_cl<U, DELTA, true, 7>(a, n, s); return;
+        default: break;
+      }
+    }
+    fm2_launch_cl<U, DELTA, true, 0>(a, n, s);
+  } else {
+    fm2_launch_cl<U, DELTA, false, 0>(a, n, s);
+  }
 }
 
 template <int U, int DELTA, bool IN_F16, bool ALIAS, int NW>
@@ -814,6 +853,7 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
   if (down != 2 || td != 12 || tu != 6 * up || (up != 2 && up != 4) || a.bias != nullptr || a.c_p % 16 != 0)
     return IC2_E_UNSUPPORTED;
   if ((int64_t)a.in_h * a.in_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // 32-bit buffer offsets
+  if (a.xsc != 1 || a.xsx % 8 != 0) return IC2_E_UNSUPPORTED;  // 16-B chunks of 8 channels
   // the wide (16 x 32) tile for the f16-input synthesis path unless IC2_FLR_WIDE=0
   static const bool wide = [] {
     const char* e = getenv("IC2_FLR_WIDE");

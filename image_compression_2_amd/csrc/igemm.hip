@@ -71,7 +71,7 @@ struct IgCfg {
 };
 
 // y = act(acc * oscale[n][o] + bias[o]) * out_mul for the channels ob .. ob+3 of output pixel p = (nn, pix),
-// stored NHWC (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only).
+// stored NHWC / NHWC16 (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only).
 __device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4]) {
   float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), bi = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.oscale) sc = *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob);
@@ -84,8 +84,12 @@ __device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int
     if (a.act) t = lrelu_gain_clamp(t, a.slope, a.act_gain, a.clamp);
     v[r] = t * a.out_mul;
   }
-  if (a.out_layout == IC2_LAYOUT_NHWC) {
-    const int64_t e = (int64_t)p * a.cout_p + ob;
+  if (a.out_layout != IC2_LAYOUT_NCHW) {
+    // NHWC, or channel-blocked NHWC16 [n][cout_p / 16][ho][wo][16] (the fused filtered lrelu's input: its
+    // 16-channel tiles read contiguous rows)
+    const int64_t e = a.out_layout == IC2_LAYOUT_NHWC
+                          ? (int64_t)p * a.cout_p + ob
+                          : (((int64_t)nn * (a.cout_p >> 4) + (ob >> 4)) * ((int64_t)a.ho * a.wo) + pix) * 16 + (ob & 15);
     if (a.out_dtype == IC2_BF16) {
       uint2 pk;
       pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -1228,16 +1232,16 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                                  void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
   IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_igemm: bad dtype %d", dtype);
-  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout == IC2_LAYOUT_NHWC),
+  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
                 "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
                 "conv_igemm: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
   IC2_CHECK_ARG(n > 0 && h > 0 && w_ > 0 && kh > 0 && kw > 0 && pad >= 0, "conv_igemm: bad geometry");
   IC2_CHECK_ARG(ho == h + 2 * pad - kh + 1 && wo == w_ + 2 * pad - kw + 1,
                 "conv_igemm: output size %dx%d does not match input %dx%d, k=%dx%d, pad=%d", ho, wo, h, w_, kh, kw, pad);
-  IC2_CHECK_ARG(out_layout == IC2_LAYOUT_NHWC || (out_layout == IC2_LAYOUT_NCHW && out_dtype == IC2_F32 &&
-                                                  cout_valid > 0 && cout_valid <= cout_p),
-                "conv_igemm: NCHW output needs f32 and 0 < cout_valid <= cout_p");
+  IC2_CHECK_ARG(out_layout == IC2_LAYOUT_NHWC || out_layout == IC2_LAYOUT_NHWC16 ||
+                    (out_layout == IC2_LAYOUT_NCHW && out_dtype == IC2_F32 && cout_valid > 0 && cout_valid <= cout_p),
+                "conv_igemm: NCHW output needs f32 and 0 < cout_valid <= cout_p (layout %d)", out_layout);
   IC2_CHECK_ARG(((uintptr_t)oscale | (uintptr_t)bias | (uintptr_t)workspace) % 16 == 0,
                 "conv_igemm: oscale/bias/workspace must be 16-byte aligned");
   const int64_t M = (int64_t)n * ho * wo;

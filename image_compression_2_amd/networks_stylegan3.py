@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import scipy.signal
@@ -33,6 +34,9 @@ import torch.nn.functional as F
 from . import _native as nv
 from . import autograd_ops as ao
 from . import sg3_ops
+
+# conv -> filtered lrelu hand-off in the channel-blocked NHWC16 layout (bf16 mode); IC2_FLR_BLOCKED=0: plain NHWC
+_FLR_BLOCKED = os.environ.get("IC2_FLR_BLOCKED", "1") != "0"
 
 
 def _train_mode(module, *tensors):
@@ -350,25 +354,33 @@ class SynthesisLayer(torch.nn.Module):
                           nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW,
                           stream, x.device)
             return out
-        # bf16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16
+        # bf16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16, in
+        # the channel-blocked layout [n][cout_p/16][conv][conv][16] the fused kernel's 16-channel tiles read as
+        # contiguous rows (IC2_FLR_BLOCKED=0: plain NHWC)
         ydt = torch.float16 if dt == torch.bfloat16 else dt
-        y = torch.empty([n, conv, conv, self.cout_p], dtype=ydt, device=x.device)
+        blocked = ydt == torch.float16 and _FLR_BLOCKED
+        if blocked:
+            y = torch.empty([n, self.cout_p // 16, conv, conv, 16], dtype=ydt, device=x.device)
+        else:
+            y = torch.empty([n, conv, conv, self.cout_p], dtype=ydt, device=x.device)
         nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
                       self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
-                      0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.device)
-        return self.flrelu_nhwc(y, dt, post_scale)
+                      0.0, 1.0, -1.0, 1.0, nv.NHWC16 if blocked else nv.NHWC, stream, x.device)
+        return self.flrelu_nhwc(y, dt, post_scale, blocked=blocked)
 
-    def flrelu_nhwc(self, y, dt_out, post_scale=None):
+    def flrelu_nhwc(self, y, dt_out, post_scale=None, blocked=False):
         """The layer's filtered lrelu on the conv output y NHWC [n, conv, conv, cout_p] (f32, or f16 for the
-        MFMA kernel) -> NHWC [n, out, out, cout_p] dt_out, times post_scale [n][cout_p] when given."""
-        n, conv = y.shape[0], y.shape[1]
+        MFMA kernel; blocked: f16/bf16 [n, cout_p/16, conv, conv, 16]) -> NHWC [n, out, out, cout_p] dt_out, times
+        post_scale [n][cout_p] when given."""
+        n, conv = y.shape[0], y.shape[2 if blocked else 1]
         s_out = int(self.out_size[0])
         out = torch.empty([n, s_out, s_out, self.cout_p], dtype=dt_out, device=y.device)
         fu = self._fu
         fd = self._fd
         px0, px1, py0, py1 = self.padding
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
-        nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(y.dtype), nv.dtype_code(dt_out), n,
+        nv.call("ic2_flrelu_nhwc16" if blocked else "ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.dtype_code(y.dtype),
+                nv.dtype_code(dt_out), n,
                 self.cout_p, conv, conv, s_out, s_out, None if fu is None else fu.ctypes.data_as(ctypes.c_void_p),
                 1 if fu is None else fu.shape[0], None if fd is None else fd.ctypes.data_as(ctypes.c_void_p),
                 1 if fd is None else fd.shape[0], None, self.up_factor, self.down_factor, px0, px1, py0, py1,

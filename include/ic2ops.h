@@ -26,7 +26,8 @@ extern "C" {
 enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
 enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 };
 enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
-enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1 };
+/* NHWC16: channel-blocked NHWC, [n][c_p / 16][h][w][16] (the synthesis conv -> fused filtered lrelu hand-off) */
+enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1, IC2_LAYOUT_NHWC16 = 2 };
 
 const char* ic2_last_error(void);
 int ic2_abi_version(void);
@@ -97,6 +98,16 @@ int ic2_flrelu_nhwc(const void* x, void* y, int dtype_in, int dtype_out, int n, 
                     int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
                     int flip, const float* post_scale, void* stream);
 
+/* ic2_flrelu_nhwc with the input in the channel-blocked layout IC2_LAYOUT_NHWC16 ([n][c_p/16][in_h][in_w][16],
+ * f16 or bf16: what ic2_conv_igemm writes with out_layout 2), output plain NHWC bf16.  Each 16-channel tile of the
+ * fused kernel then reads contiguous rows instead of 32 B out of every c_p*2-byte pixel.  Same semantics as
+ * ic2_flrelu_nhwc (SynthesisLayer's filtered_lrelu, SG3-public; called at stylegan3_hvae_full.py:274,329);
+ * configurations without an MFMA instance return IC2_E_UNSUPPORTED. */
+int ic2_flrelu_nhwc16(const void* x, void* y, int dtype_in, int dtype_out, int n, int c_p, int in_h, int in_w,
+                      int out_h, int out_w, const float* fu, int fu_taps, const float* fd, int fd_taps, const float* b,
+                      int up, int down, int px0, int px1, int py0, int py1, float gain, float slope, float clamp,
+                      int flip, const float* post_scale, void* stream);
+
 /* ----------------------------------------------------------------- modulated conv (MFMA) ---- */
 
 /* FullyConnectedLayer.forward [SG3-public] and nn.Linear (stylegan3_hvae_full.py:206-234):
@@ -123,7 +134,8 @@ int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int 
 /* NHWC implicit-GEMM convolution on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32):
  *   acc[n,p,o] = sum_{ky,kx,i} w[o][ky][kx][i] * x[n, p + (ky,kx) - pad, i]   (zero outside the image)
  *   v = acc * (oscale ? oscale[n][o] : 1) + (bias ? bias[o] : 0);  if act: v = clamp(lrelu(v)*act_gain)
- *   y = v * out_mul  -> NHWC [n][ho][wo][cout_p] (layout 0) or NCHW f32 [n][cout_valid][ho][wo] (layout 1).
+ *   y = v * out_mul  -> NHWC [n][ho][wo][cout_p] (layout 0), NCHW f32 [n][cout_valid][ho][wo] (layout 1) or
+ *   channel-blocked NHWC16 [n][cout_p/16][ho][wo][16] (layout 2, any out dtype).
  * Replaces the grouped conv2d of modulated_conv2d [SG3-public] and nn.Conv2d of VGGBlock
  * (stylegan3_hvae_full.py:175-176) / from_rgb (:62).  cin_p, cout_p multiples of 32. */
 int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,

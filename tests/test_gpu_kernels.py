@@ -227,6 +227,65 @@ def test_flrelu_nhwc_bf16_matches_oracle(cuda, gen256_bf16_layers, layer, c_p, i
     assert err.mean().item() < 2e-3 * (1 + r.abs().mean().item())
 
 
+@pytest.mark.parametrize("layer", [0, 2, 6, 8, 10, 13])
+@pytest.mark.parametrize("c_p", [32, 64])
+def test_flrelu_nhwc16_equals_nhwc(cuda, gen256_bf16_layers, layer, c_p):
+    """The channel-blocked hand-off (ic2_flrelu_nhwc16 on [n][c_p/16][h][w][16]) only changes the addressing of
+    the fused kernel's input tiles: its output is bit-identical to ic2_flrelu_nhwc on the same values in NHWC
+    (narrow and wide tiles, up 2 and up 4, both paddings), post_scale included."""
+    import ctypes
+    L = gen256_bf16_layers[layer]
+    n = 2
+    conv = int(L.in_size[0]) + 2
+    s_out = int(L.out_size[0])
+    g = torch.Generator().manual_seed(60 + layer)
+    x = (torch.randn(n, conv, conv, c_p, generator=g) * 2).to(torch.float16)
+    x[:, :4, :6, :] = 300.0
+    ps = (torch.rand(n, c_p, generator=g) + 0.5).to(cuda)
+    xd = x.to(cuda)
+    xb = x.reshape(n, conv, conv, c_p // 16, 16).permute(0, 3, 1, 2, 4).contiguous().to(cuda)
+    outs = []
+    for fn, src in (("ic2_flrelu_nhwc", xd), ("ic2_flrelu_nhwc16", xb)):
+        out = torch.full((n, s_out, s_out, c_p), float("nan"), device=cuda, dtype=torch.bfloat16)
+        nv.call(fn, nv.ptr(src), nv.ptr(out), nv.F16, nv.BF16, n, c_p, conv, conv, s_out, s_out,
+                L._fu.ctypes.data_as(ctypes.c_void_p), L._fu.shape[0], L._fd.ctypes.data_as(ctypes.c_void_p),
+                L._fd.shape[0], None, L.up_factor, L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0,
+                nv.ptr(ps), nv.stream_of(src))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout,size,n", [(512, 512, 12, 2), (512, 362, 20, 2), (256, 192, 40, 2),
+                                             (192, 128, 66, 2), (128, 128, 70, 1), (96, 64, 48, 2), (32, 64, 40, 2)])
+def test_conv_nhwc16_equals_nhwc(cuda, cin, cout, size, n):
+    """ic2_conv_igemm with out_layout NHWC16 (f16, the synthesis conv -> filtered-lrelu hand-off) stores exactly the
+    values of the NHWC output, channel-blocked, for whichever kernel the launch plan picks (8-phase GEMM, halo
+    GEMM, halo conv, plain / split-K implicit GEMM); padded output channels included."""
+    cin_p, cout_p = nv.pad_synth(cin), nv.pad_synth(cout)
+    g = torch.Generator().manual_seed(cin + cout + size)
+    x = torch.zeros(n, size, size, cin_p)
+    x[..., :cin] = torch.randn(n, size, size, cin, generator=g)
+    w = torch.zeros(cout_p, 3, 3, cin_p)
+    w[:cout, :, :, :cin] = torch.randn(cout, 3, 3, cin, generator=g) / np.sqrt(9 * cin)
+    osc = (torch.rand(n, cout_p, generator=g) + 0.5).to(cuda)
+    bias = torch.randn(cout_p, generator=g).to(cuda)
+    xd, wd = x.to(cuda, torch.bfloat16), w.to(cuda, torch.bfloat16)
+    ho = size
+    ys = {}
+    for lay in (nv.NHWC, nv.NHWC16):
+        y = torch.full((n * ho * ho * cout_p,), float("nan"), device=cuda, dtype=torch.float16)
+        nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), nv.BF16, nv.F16, n, size, size, cin_p, cout_p, cout, 3, 3, 1,
+                      ho, ho, nv.ptr(osc), nv.ptr(bias), 0, 0.0, 1.0, -1.0, 1.0, lay, nv.stream_of(xd), cuda)
+        ys[lay] = y
+    torch.cuda.synchronize()
+    a = ys[nv.NHWC].view(n, ho, ho, cout_p)
+    b = ys[nv.NHWC16].view(n, cout_p // 16, ho, ho, 16).permute(0, 2, 3, 1, 4).reshape(n, ho, ho, cout_p)
+    assert torch.isfinite(a.float()).all()
+    assert torch.equal(a, b)
+
+
 def test_f16_saturation_semantics(cuda, gen256_bf16_layers):
     """bf16 mode hands the filtered lrelu the modulated-conv output as f16 (its MFMA operand type), so a
     pre-activation beyond +-65504 saturates BEFORE the up-FIR, while the reference's fp32 CPU path clamps (at

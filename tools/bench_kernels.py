@@ -30,10 +30,13 @@ def child(kind):
         s_out = int(L.out_size[0])
         if kind == "flr":
             # f16 input: what the synthesis conv epilogue hands the fused filtered lrelu
+            # (channel-blocked NHWC16, as the synthesis path hands it over, unless IC2_FLR_BLOCKED=0)
+            blocked = os.environ.get("IC2_FLR_BLOCKED", "1") != "0"
             y = (torch.randn(n, conv, conv, L.cout_p, device=dev) * 2).to(torch.float16)
             out = torch.empty(n, s_out, s_out, L.cout_p, device=dev, dtype=torch.bfloat16)
+            fn = "ic2_flrelu_nhwc16" if blocked else "ic2_flrelu_nhwc"
             def run():
-                nv.call("ic2_flrelu_nhwc", nv.ptr(y), nv.ptr(out), nv.F16, nv.BF16, n, L.cout_p, conv, conv, s_out,
+                nv.call(fn, nv.ptr(y), nv.ptr(out), nv.F16, nv.BF16, n, L.cout_p, conv, conv, s_out,
                         s_out, L._fu.ctypes.data_as(__import__("ctypes").c_void_p), L._fu.shape[0],
                         L._fd.ctypes.data_as(__import__("ctypes").c_void_p), L._fd.shape[0], None, L.up_factor,
                         L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0, None, nv.stream_of(y))
