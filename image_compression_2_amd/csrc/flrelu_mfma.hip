@@ -27,6 +27,7 @@ typedef _Float16 fm_h8 __attribute__((ext_vector_type(8)));
 typedef short fm_s4 __attribute__((ext_vector_type(4)));
 typedef float fm_f4 __attribute__((ext_vector_type(4)));
 typedef float fm_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
 
 constexpr int FM_TAPS = 276;
 constexpr uint32_t FM_OOB = 0x7ffffff0u;  // buffer num_records = the zero-answer offset (per-sample image < 2 GiB)
@@ -70,6 +71,16 @@ __device__ constexpr int fm_win(int i) {
 
 __device__ __forceinline__ fm_s4 fm_tr_read(const uint32_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) fm_s4*)p);
+}
+
+// LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds: lane l's bytes land at lds_dst + 16 l) issued from inline
+// asm: the compiler then does not know an LDS write is in flight and inserts no vmcnt(0) in front of the next LDS
+// read of an unrelated buffer (which it does for the builtin, turning a prefetch into a synchronous load).  The
+// caller waits for it with an explicit s_waitcnt vmcnt before a barrier.
+__device__ __forceinline__ void fm_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, const uint32_t* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)lds_dst);
+  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(m0) : "memory");
 }
 
 // f32 -> f16 pairs (v_cvt_pk_f16_f32, round to nearest even)
@@ -474,7 +485,8 @@ struct FmGeom2 {
   static constexpr int D_XP = 10;
   static constexpr int D_PITCH = TOX * D_XP + 8;
   static constexpr int D_DW = 16 * D_PITCH;
-  static constexpr int LDS_DW = IN_DW + V_DW + (D_DW > FM_TAPS ? D_DW : FM_TAPS);
+  static constexpr int DT_DW = D_DW > FM_TAPS ? D_DW : FM_TAPS;  // D image, aliased by the tap table
+  static constexpr int LDS_DW = IN_DW + V_DW + DT_DW + 16;       // + the tile's 16 post-scale floats
   static_assert(NINX % 2 == 1 && NINY % 2 == 1 && NINY >= 16, "input image sides must be odd and cover a window");
   static_assert(NBX == 2 * NOB + 1, "horizontal down: output block ob reads grid blocks 2ob .. 2ob+2");
 };
@@ -489,6 +501,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   uint32_t* const v_img = lds + G::IN_DW;
   uint32_t* const d_img = v_img + G::V_DW;
   float* const taps = reinterpret_cast<float*>(d_img);  // read only before the first tile
+  uint32_t* const ps_lds = d_img + G::DT_DW;             // the tile's post-scale row (DMA'd with its input)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -545,9 +558,13 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
         const int iy = sy0 + (yx & 0xffff), ix = sx0 + (yx >> 16);
         const bool ok = yx >= 0 && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
         const uint32_t off = ok ? (uint32_t)((iy * xsy + ix * xsx + half8) * 2) : FM_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(in_img + k * 256), 16,
-                                                 off, 0, 0, 0);
+        fm_dma16(rs, off, in_img + k * 256);
       }
+    }
+    if (a.post_scale != nullptr && wave == NW - 1 && lane < 4) {  // 64 B: post_scale[n][c0 .. c0 + 16)
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.post_scale + (int64_t)n * a.c_p + c0), 0, 64, 0x00020000);
+      fm_dma16(prs, lane * 16, ps_lds);
     }
   };
   if (slot < ntiles) load_tile(slot);
@@ -619,8 +636,14 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   for (int t = slot; t < ntiles; t += gridDim.x) {
     int n, oy0, ox0, c0;
     tile_geom(t, n, oy0, ox0, c0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA (and last tile's stores)
-    __syncthreads();                                   // everyone's; and the previous tile fully consumed
+    // this wave's LDS-DMA of the tile; the previous tile's OCW output stores (issued after that DMA, always
+    // exactly OCW: out-of-range ones are dropped by the buffer bounds, not branched around) stay in flight
+    if (t == slot) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
+    __syncthreads();  // everyone's DMA; and the previous tile fully consumed
+    // the post-scale row came with the DMA; into registers before the next tile's DMA overwrites it
+    float4 psv = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (a.post_scale) psv = *reinterpret_cast<const float4*>(ps_lds + 4 * g);
 
     fm_f4 acc[OCW];
 #pragma unroll
@@ -725,21 +748,20 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
       }
     }
 
-    // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox)
-    float ps[4] = {1.f, 1.f, 1.f, 1.f};
-    if (a.post_scale) {
-      const float4 p = *reinterpret_cast<const float4*>(a.post_scale + (int64_t)n * a.c_p + c0 + 4 * g);
-      ps[0] = p.x; ps[1] = p.y; ps[2] = p.z; ps[3] = p.w;
-    }
+    // ---- store: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox); buffer stores with
+    // the per-sample image as the resource, out-of-range pixels at the dropped offset FM_OOB
+    const float ps[4] = {psv.x, psv.y, psv.z, psv.w};
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(yout + (int64_t)n * a.out_h * a.out_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
     const int gy = oy0 + li;
 #pragma unroll
     for (int i = 0; i < OCW; ++i) {
       const int gx = ox0 + wave + NW * i;
-      if (gy < a.out_h && gx < a.out_w) {
-        const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
-                                   (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
-        *reinterpret_cast<uint2*>(yout + (((int64_t)n * a.out_h + gy) * a.out_w + gx) * a.c_p + c0 + 4 * g) = v;
-      }
+      const uint32_t off = (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
+      const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
+                                 (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
+      if constexpr (!(ABL & 8))
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, off, 0, 0);
     }
   }
 }
@@ -772,7 +794,7 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
     return !(e && e[0] == '0');
   }();
   // IC2_FLR_ABL (diagnostic, gives WRONG results): bit 1 drops the in-tile barriers, 2 the activation VALU, 4 the
-  // input DMA, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
+  // input DMA, 8 the output stores, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
   static const int abl = [] {
     const char* e = getenv("IC2_FLR_ABL");
     return e ? atoi(e) : 0;
@@ -783,6 +805,8 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
         case 1: fm2_launch_cl<U, DELTA, true, 1>(a, n, s); return;
         case 2: fm2_launch_cl<U, DELTA, true, 2>(a, n, s); return;
         case 4: fm2_launch_cl<U, DELTA, true, 4>(a, n, s); return;
+        case 8: fm2_launch_cl<U, DELTA, true, 8>(a, n, s); return;
+        case 12: fm2_launch_cl<U, DELTA, true, 12>(a, n, s); return;
         case 16: fm2_launch_cl<U, DELTA, true, 16>(a, n, s); return;
         case 32: fm2_launch_cl<U, DELTA, true, 32>(a, n, s); return;
         case 7: fm2_launch_cl<U, DELTA, true, 7>(a, n, s); return;
@@ -854,6 +878,7 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
     return IC2_E_UNSUPPORTED;
   if ((int64_t)a.in_h * a.in_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // 32-bit buffer offsets
   if (a.xsc != 1 || a.xsx % 8 != 0) return IC2_E_UNSUPPORTED;  // 16-B chunks of 8 channels
+  if ((int64_t)a.out_h * a.out_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // output offsets too
   // the wide (16 x 32) tile for the f16-input synthesis path unless IC2_FLR_WIDE=0
   static const bool wide = [] {
     const char* e = getenv("IC2_FLR_WIDE");
