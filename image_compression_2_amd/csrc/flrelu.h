@@ -17,6 +17,7 @@ struct FlrArgs {
   int in_h, in_w, out_h, out_w;
   int py0, px0;                 // leading padding
   int tiles_x, tiles_y, cblocks, nimg;
+  int order;  // wide MFMA kernel: tile order, 0 = channel block fastest, 1 = x, y fastest (one plane per XCD run)
   float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
   float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
   float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)

@@ -517,15 +517,34 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
     taps[i] = v;
   }
 
-  const int slot = fm_xcd_remap(blockIdx.x, gridDim.x);
+  // persistent tile walk.  order 0 / 1: slot, slot + G, ... over the XCD-remapped grid (consecutive slots on one
+  // XCD).  order 2: XCD x walks its own contiguous eighth of the tiles in raster order (one or a few samples),
+  // so vertically adjacent tiles, whose input halos overlap, share that XCD's L2
+  int slot = fm_xcd_remap(blockIdx.x, gridDim.x), tstep = gridDim.x, tend = ntiles;
+  if (a.order == 2) {
+    const int xcd = blockIdx.x & 7, nx = ((int)gridDim.x - xcd + 7) >> 3, chunk = (ntiles + 7) >> 3;
+    slot = xcd * chunk + (blockIdx.x >> 3);
+    tstep = nx;
+    tend = min(ntiles, (xcd + 1) * chunk);
+  }
   const uint16_t* xin = reinterpret_cast<const uint16_t*>(a.x);
   auto tile_geom = [&](int t, int& n, int& oy0, int& ox0, int& c0) {
-    const int cb = t % a.cblocks;
-    t /= a.cblocks;
-    const int tx = t % a.tiles_x;
-    t /= a.tiles_x;
-    const int ty = t % a.tiles_y;
-    n = t / a.tiles_y;
+    int cb, tx, ty;
+    if (a.order != 1) {
+      cb = t % a.cblocks;
+      t /= a.cblocks;
+      tx = t % a.tiles_x;
+      t /= a.tiles_x;
+      ty = t % a.tiles_y;
+      n = t / a.tiles_y;
+    } else {
+      tx = t % a.tiles_x;
+      t /= a.tiles_x;
+      ty = t % a.tiles_y;
+      t /= a.tiles_y;
+      cb = t % a.cblocks;
+      n = t / a.cblocks;
+    }
     oy0 = ty * 16;
     ox0 = tx * TOX;
     c0 = cb * 16;
@@ -567,7 +586,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
       fm_dma16(prs, lane * 16, ps_lds);
     }
   };
-  if (slot < ntiles) load_tile(slot);
+  if (slot < tend) load_tile(slot);
   __syncthreads();  // taps
 
   // filter matrices (f16) in registers; y and x windows differ only through NINY / NINX clipping
@@ -633,7 +652,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
   __syncthreads();  // every wave's tap reads are done before the first D store overwrites the table
 
-  for (int t = slot; t < ntiles; t += gridDim.x) {
+  for (int t = slot; t < tend; t += tstep) {
     int n, oy0, ox0, c0;
     tile_geom(t, n, oy0, ox0, c0);
     // this wave's LDS-DMA of the tile; the previous tile's OCW output stores (issued after that DMA, always
@@ -675,7 +694,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
         }
       }
       if constexpr (!(ABL & 1)) __syncthreads();
-      if (!(ABL & 4) && b == 2 && t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);  // input image dead: prefetch
+      if (!(ABL & 4) && b == 2 && t + tstep < tend) load_tile(t + tstep);  // input image dead: prefetch
       // ---- horizontal: up (NBX column blocks), activation, down (NOB output blocks), one grid row of this
       // wave at a time (bounded register pressure: 2 workgroups per CU need <= 128 VGPRs)
       if constexpr (!(ABL & 16))
@@ -757,7 +776,11 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
 #pragma unroll
     for (int i = 0; i < OCW; ++i) {
       const int gx = ox0 + wave + NW * i;
-      const uint32_t off = (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
+      uint32_t off = (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
+      if constexpr ((ABL & 64) != 0)  // diagnostic: channel-blocked output addressing (wrong layout for consumers)
+        off = (gy < a.out_h && gx < a.out_w)
+                  ? (uint32_t)((((c0 >> 4) * a.out_h + gy) * a.out_w + gx) * 32 + 8 * g) - (uint32_t)(c0 * 2)
+                  : FM_OOB;
       const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
                                  (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
       if constexpr (!(ABL & 8))
@@ -772,6 +795,12 @@ static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
   a.tiles_x = (int)ceil_div(a.out_w, TOX);
   a.tiles_y = (int)ceil_div(a.out_h, 16);
   a.cblocks = a.c_p / 16;
+  // IC2_FLR_ORDER=1: spatial tiles fastest, so the tiles one XCD runs together share their input halos in its L2
+  static const int order = [] {
+    const char* e = getenv("IC2_FLR_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  a.order = order;
   const int ntiles = n * a.tiles_y * a.tiles_x * a.cblocks;
   static int resident = 0;
   if (resident == 0) {
@@ -794,7 +823,7 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
     return !(e && e[0] == '0');
   }();
   // IC2_FLR_ABL (diagnostic, gives WRONG results): bit 1 drops the in-tile barriers, 2 the activation VALU, 4 the
-  // input DMA, 8 the output stores, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
+  // input DMA, 8 the output stores, 64 blocked output addressing, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
   static const int abl = [] {
     const char* e = getenv("IC2_FLR_ABL");
     return e ? atoi(e) : 0;
@@ -807,6 +836,7 @@ static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
         case 4: fm2_launch_cl<U, DELTA, true, 4>(a, n, s); return;
         case 8: fm2_launch_cl<U, DELTA, true, 8>(a, n, s); return;
         case 12: fm2_launch_cl<U, DELTA, true, 12>(a, n, s); return;
+        case 64: fm2_launch_cl<U, DELTA, true, 64>(a, n, s); return;
         case 16: fm2_launch_cl<U, DELTA, true, 16>(a, n, s); return;
         case 32: fm2_launch_cl<U, DELTA, true, 32>(a, n, s); return;
         case 7: fm2_launch_cl<U, DELTA, true, 7>(a, n, s); return;
