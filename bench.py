@@ -358,6 +358,9 @@ def run(args):
         comp = ic2.StyleGAN3Compressor(enc, G, training_resolution=res if train else None)
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         x = torch.rand(batch, 3, res, res, generator=g, device=dev) * 2 - 1
+        # (pixel count, image count) of the metric record: device constants made once, so the step has no
+        # host->device copy (a pageable one stalls the host until the stream drains)
+        counts = torch.tensor([float(x.numel()), float(batch)], dtype=torch.float64, device=dev)
 
         if train:
             from image_compression_2_amd import training as ict
@@ -366,8 +369,8 @@ def run(args):
 
             def train_step():
                 losses = ict.train_step(comp, x, opt, w_avg, rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01)
-                vec = torch.stack([losses["rec_loss"].double() * batch, losses["kl_loss"].double() * batch,
-                                   torch.tensor(float(batch), device=dev, dtype=torch.float64)])
+                vec = torch.cat([(losses["rec_loss"].double() * batch).view(1),
+                                 (losses["kl_loss"].double() * batch).view(1), counts[1:]])
                 return icd.allreduce_sum(vec, device=dev)
 
         def step():
@@ -377,8 +380,7 @@ def run(args):
                 if img.shape[2] != res:
                     img = ic2.resize_bilinear(img, (res, res))
                 sse = icm.uint8_sse(img, x)
-            vec = torch.stack([sse.sum(), torch.tensor(float(img.numel()), device=dev, dtype=torch.float64),
-                               torch.tensor(float(batch), device=dev, dtype=torch.float64)])
+            vec = torch.cat([sse.sum().view(1), counts])
             return icd.allreduce_sum(vec, device=dev)
 
     if not dry and args.config == "c5":

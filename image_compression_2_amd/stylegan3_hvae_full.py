@@ -289,6 +289,19 @@ class VGGBlock(nn.Module):
         return _to_nchw(self.run_nhwc(_to_nhwc(x, torch.float32, stream), torch.float32, self._cache, stream), stream)
 
 
+def _fresh_linear(in_features, out_features, device):
+    """nn.Linear(in_features, out_features) initialised on the CPU generator exactly as the reference's
+    per-call re-creation (:225-230) and moved to `device` without a host sync: the parameters go through pinned
+    memory with non_blocking copies (a pageable copy would block the host until the stream drained, leaving the
+    GPU idle while the host then issues the synthesis launches one by one)."""
+    lin = nn.Linear(in_features, out_features)
+    if device.type == "cuda":
+        with torch.no_grad():
+            for prm in lin.parameters():
+                prm.data = prm.data.pin_memory().to(device, non_blocking=True)
+    return lin
+
+
 class HierarchyProjector(nn.Module):
     """GAP -> fc1 -> lrelu -> fc2 -> (mean, logvar) -> reparameterise (ref ``:194-247``)."""
 
@@ -307,7 +320,7 @@ class HierarchyProjector(nn.Module):
         n, in_features = pooled.shape
         if in_features != self.in_channels:
             # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
-            self.fc1 = nn.Linear(in_features, 256).to(pooled.device)
+            self.fc1 = _fresh_linear(in_features, 256, pooled.device)
         h = _linear(self.fc1, pooled, stream, act=True, slope=self.act.negative_slope)
         p = _linear(self.fc2, h, stream)
         # torch.randn_like(std) on the device, in the reference's order (global, medium, fine)
@@ -321,7 +334,7 @@ class HierarchyProjector(nn.Module):
         n, in_features = pooled.shape
         if in_features != self.in_channels:
             # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
-            self.fc1 = nn.Linear(in_features, 256).to(pooled.device)
+            self.fc1 = _fresh_linear(in_features, 256, pooled.device)
         h = F.leaky_relu(F.linear(pooled, self.fc1.weight, self.fc1.bias), self.act.negative_slope)
         p = F.linear(h, self.fc2.weight, self.fc2.bias).view(n, self.num_ws, self.w_dim * 2)
         mean, logvar = torch.chunk(p, 2, dim=2)
