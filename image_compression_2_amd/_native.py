@@ -42,6 +42,7 @@ _SIGS = {
     "ic2_fc": [_P, _I64, _P, _P, _P, _I, _I, _I, _F, _F, _I, _F, _F, _P],
     "ic2_pack_weight": [_P, _I, _I, _I, _I, _I, _I, _I, _F, _P, _I, _P, _P],
     "ic2_modconv_prep": [_P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P],
+    "ic2_modconv_prep_batched": [_P, _I64, _I, _I, _I, _P, _P],
     "ic2_conv_igemm": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I,
                        _P],
     "ic2_conv_igemm_ws_bytes": [_I, _I, _I, _I, _I, _I, _I, _I, _I],

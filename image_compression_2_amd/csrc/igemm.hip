@@ -70,12 +70,26 @@ struct IgCfg {
   __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
 };
 
+// Per-channel epilogue operands.  The epilogues load them for all their channel blocks BEFORE the first store: a
+// load placed after a store to y may alias it, so loading inside the store loop serialised one load round trip per
+// 16 x 16 block (33 `s_waitcnt vmcnt(0)` per wave in the 8-phase and halo kernels' epilogues).
+__device__ __forceinline__ float4 ig_load_oscale(const IgemmArgs& a, int nn, int ob) {
+  return a.oscale && ob < a.cout_p ? *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob)
+                                   : make_float4(1.f, 1.f, 1.f, 1.f);
+}
+__device__ __forceinline__ float4 ig_load_bias(const IgemmArgs& a, int ob) {
+  return a.bias && ob < a.cout_p ? *reinterpret_cast<const float4*>(a.bias + ob) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// Retire the preloads with a real s_waitcnt vmcnt(0) (gfx9 encoding: expcnt / lgkmcnt left at their maxima), so the
+// waitcnt pass sees them complete; otherwise it re-waits vmcnt(0) -- behind the previous block's stores -- at
+// every join of the branchy store code below.
+__device__ __forceinline__ void ig_preloads_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // y = act(acc * oscale[n][o] + bias[o]) * out_mul for the channels ob .. ob+3 of output pixel p = (nn, pix),
-// stored NHWC / NHWC16 (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only).
-__device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4]) {
-  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), bi = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.oscale) sc = *reinterpret_cast<const float4*>(a.oscale + (int64_t)nn * a.cout_p + ob);
-  if (a.bias) bi = *reinterpret_cast<const float4*>(a.bias + ob);
+// stored NHWC / NHWC16 (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only); sc / bi = the preloaded
+// oscale[nn][ob..ob+3] / bias[ob..ob+3].
+__device__ __forceinline__ void ig_store4v(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4],
+                                           float4 sc, float4 bi) {
   const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, biv[4] = {bi.x, bi.y, bi.z, bi.w};
   float v[4];
 #pragma unroll
@@ -115,6 +129,9 @@ __device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int
       if (ob + r < a.cout_valid) yo[((int64_t)nn * a.cout_valid + ob + r) * hw + pix] = v[r];
   }
 }
+__device__ __forceinline__ void ig_store4(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4]) {
+  ig_store4v(a, p, nn, pix, ob, acc, ig_load_oscale(a, nn, ob), ig_load_bias(a, ob));
+}
 
 // Epilogue shared by the kernels: lane holds C[o = obase + 16i + 4*fh + r][p = pbase + 16j + fr].
 // A split-K slice (gridDim.y > 1) stores its raw partial sums instead.
@@ -122,23 +139,41 @@ template <int I, int J>
 __device__ __forceinline__ void ig_epilogue(const IgemmArgs& a, const f32x4 (&acc)[I][J], int obase, int pbase, int fr,
                                             int fh) {
   const int hw = a.ho * a.wo;
-  const bool partial = gridDim.y > 1;
+  if (gridDim.y > 1) {  // split-K slice: raw partial sums
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int p = pbase + j * 16 + fr;
+      if (p >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int ob = obase + i * 16 + 4 * fh;
+        if (ob < a.cout_p) *reinterpret_cast<f32x4*>(a.ws + ((int64_t)blockIdx.y * a.M + p) * a.cout_p + ob) = acc[i][j];
+      }
+    }
+    return;
+  }
+  // bias for every channel block, then per 16-pixel column the oscale rows of its samples (a wave's pixels may
+  // span two samples), loaded before that column's stores
+  float4 bi[I];
+#pragma unroll
+  for (int i = 0; i < I; ++i) bi[i] = ig_load_bias(a, obase + i * 16 + 4 * fh);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int p = pbase + j * 16 + fr;
+    const int pc = p < a.M ? p : a.M - 1;
+    const int nn = pc / hw;
+    const int pix = pc - nn * hw;
+    float4 sc[I];
+#pragma unroll
+    for (int i = 0; i < I; ++i) sc[i] = ig_load_oscale(a, nn, obase + i * 16 + 4 * fh);
+    ig_preloads_done();
     if (p >= a.M) continue;
-    const int nn = p / hw;
-    const int pix = p - nn * hw;
 #pragma unroll
     for (int i = 0; i < I; ++i) {
       const int ob = obase + i * 16 + 4 * fh;
       if (ob >= a.cout_p) continue;
-      if (partial) {
-        *reinterpret_cast<f32x4*>(a.ws + ((int64_t)blockIdx.y * a.M + p) * a.cout_p + ob) = acc[i][j];
-        continue;
-      }
       const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      ig_store4(a, p, nn, pix, ob, v);
+      ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
     }
   }
 }
@@ -781,6 +816,13 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
 
   // epilogue: lane holds C[o = o0 + obase + 16 i + 4 fh + r][tile pixel (pb, fr)]
   const int hw = a.ho * a.wo;
+  float4 sc[8], bi[8];  // one sample per tile: every channel block's operands before the first store
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = ig_load_oscale(a, nn, o0 + obase + i * 16 + 4 * fh);
+    bi[i] = ig_load_bias(a, o0 + obase + i * 16 + 4 * fh);
+  }
+  ig_preloads_done();
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int pb = pg * J + j;
@@ -793,7 +835,7 @@ __device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int 
       const int ob = o0 + obase + i * 16 + 4 * fh;
       if (ob >= a.cout_p) continue;
       const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      ig_store4(a, p, nn, pix, ob, v);
+      ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
     }
   }
 }
@@ -853,6 +895,285 @@ static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int
   if (mode == 2) return true;
   const double util = (double)ho * wo * n * ceil_div(cout_p, p.og2 ? 256 : 128) / (256.0 * p.blocks);
   return cin_p <= 256 && cout_p <= 256 && util >= 0.95;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Halo implicit GEMM, 4-wave form (`hg4`): the same halo idea as hgemm above, shaped for two workgroups per CU.
+// hgemm runs ONE 8-wave workgroup per CU whose waves all meet at the per-K-step barrier, so the two waves of a
+// SIMD read their fragments at the same time and then compete for the matrix pipe at the same time (MFMA busy
+// 0.30-0.38 on the 128 / 192-wide SG3 layers, profiles/r2_pmc_shapes_c2_bf16_b32.json).  Here a workgroup is
+// 4 waves (one per SIMD) and needs <= 74 KB of LDS, so two independent workgroups share each CU and one's
+// barrier / fragment-read phase overlaps the other's MFMAs without any ping-pong bookkeeping.
+//   K-step = one tap x 32 channels (64-B LDS rows); wave tile (16 I) o x (16 J) px, 2 fragments per MFMA pair
+//   read per step: I + J ds_read_b128 for I*J MFMAs (8 + 4 for 32 at the 128 x 256 tile: 12 KB per wave and
+//   step, 40 % less LDS read traffic per MFMA than hgemm's 128 x 32 wave tile at 64 channels).
+//   Weights stream through a 3-slab ring (the slab for step t+2 is issued at step t, so a DMA has a whole step
+//   plus the barrier to land); the next 32-channel block's halo is spread over the first taps of the current
+//   block, one 1-KiB DMA per wave per step, so every step waits for the same small count (vmcnt(NWI [+1])).
+//   LDS rows of 64 B, 16-B chunk c stored at c ^ (((row >> 2) & 1) << 1): conflict-free ds_read_b128 for 16
+//   consecutive rows starting at ANY row (the halo fragments start at tap-shifted rows), checked by brute force
+//   over the four ds_read_b128 lane groups.
+template <int I, int J, int WGO, int WGP, int TW, int NS>
+struct H4 {
+  static constexpr int BO = 16 * I * WGO, BP = 16 * J * WGP, TH = BP / TW;
+  static constexpr int HW = TW + 2, HH = TH + 2, NH = HH * HW;  // halo pixels
+  static constexpr int NHI = (NH + 15) / 16;                    // 1-KiB DMA instructions per halo (16 px)
+  static constexpr int HPW = (NHI + 3) / 4;                     // per wave, at most
+  static constexpr int HALO_B = NHI * 1024;
+  static constexpr int WS_B = BO * 64;                          // one weight slab: BO rows x 32 channels
+  static constexpr int NWI = (BO / 16 + 3) / 4;                 // weight DMA instructions per wave
+  static constexpr int LDS_B = NS * WS_B + 2 * HALO_B;  // NS-slab weight ring
+  static_assert(BP % TW == 0 && TW % 16 == 0, "pixel tile");
+  static_assert((BO / 16) % 4 == 0, "weight slab rows split evenly over the 4 waves");
+  static_assert(HPW <= 8, "halo DMA spread over the first 8 taps");
+  static_assert(LDS_B <= 80 * 1024, "two workgroups per CU");
+};
+__device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
+
+template <int I, int J, int WGO, int WGP, int TW, int NS>
+__device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
+  using G = H4<I, J, WGO, WGP, TW, NS>;
+  constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
+  constexpr int NWI = G::NWI, HPW = G::HPW;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
+  char* const wsl = lds;                    // NS weight slabs
+  char* const hal = lds + NS * G::WS_B;     // 2 halos
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int og = wid / WGP, pg = wid % WGP;
+  const int fr = lane & 15, fh = lane >> 4;
+
+  const int logical = xcd_remap(blockIdx.x, a.nblocks);
+  const int o_tile = logical % a.tiles_o;
+  int pt = logical / a.tiles_o;
+  const int tx = pt % tiles_x;
+  pt /= tiles_x;
+  const int ty = pt % tiles_y;
+  const int nn = pt / tiles_y;
+  const int o0 = o_tile * G::BO;
+  const int oy0 = ty * G::TH, ox0 = tx * TW;
+
+  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
+  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
+  const int lrow = lane >> 2, pch = lane & 3;  // DMA: 16 rows x 4 chunks of 16 B per instruction
+
+  uint32_t w_off[NWI];
+#pragma unroll
+  for (int k = 0; k < NWI; ++k) {
+    const int row = (wid + 4 * k) * 16 + lrow;
+    const int o = o0 + row;
+    w_off[k] = (row < G::BO && o < a.cout_p) ? (uint32_t)(o * a.K * 2 + ((pch ^ (((row >> 2) & 1) << 1)) << 4)) : kOob;
+  }
+  uint32_t h_off[HPW];
+#pragma unroll
+  for (int k = 0; k < HPW; ++k) {
+    const int g = wid + 4 * k;
+    const int hp = g * 16 + lrow;
+    const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
+    const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
+    const bool ok = g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
+    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ (((hp >> 2) & 1) << 1)) << 3)) * 2)
+                  : kOob;
+  }
+  int brow[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pb = pg * J + j;
+    brow[j] = (pb * 16 / TW) * G::HW + (pb * 16) % TW + fr;
+  }
+  const int obase = og * 16 * I;
+  const bool live = o0 + obase < a.cout_p;
+  const int CB = a.cin_p >> 5;
+  const int nq = CB * 9;
+
+  auto issue_w = [&](int t) {  // weight slab of K-step t -> slab t % NS
+    const int cb = t / 9, tap = t - (t / 9) * 9;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(wg + ((int64_t)tap * a.cin_p + cb * 32) * 2), 0, t < nq ? kOob : 0, kRsrcWord3);
+    char* dst = wsl + (t % NS) * G::WS_B;
+#pragma unroll
+    for (int k = 0; k < NWI; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 4 * k) * 1024),
+                                               16, w_off[k], 0, 0, 0);
+  };
+  auto issue_h1 = [&](int cb, int k) {  // DMA k of this wave for the halo of block cb -> halo cb & 1
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 64), 0, kOob, kRsrcWord3);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(hal + (cb & 1) * G::HALO_B + (wid + 4 * k) * 1024), 16, h_off[k],
+        0, 0, 0);
+  };
+
+  f32x4 acc[I][J];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int k = 0; k < HPW; ++k)
+    if (wid + 4 * k < G::NHI) issue_h1(0, k);
+#pragma unroll
+  for (int t = 0; t < LA; ++t) issue_w(t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");  // halo 0 and slab 0 landed
+  for (int t = 0; t < nq; ++t) {
+    __builtin_amdgcn_s_barrier();  // slab t and block t/9's halo landed for every wave; step t-1's reads done
+    __builtin_amdgcn_sched_barrier(0);
+    const int cb = t / 9, tap = t - (t / 9) * 9;
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    issue_w(t + LA);  // slab (t+LA) % NS was last read by step t-1
+    // one DMA of the next block's halo per step over the block's first taps (halo (cb+1) & 1 was last read
+    // by block cb-1); wave-uniform condition
+    const bool hdma = tap < HPW && cb + 1 < CB && wid + 4 * tap < G::NHI;
+    if (hdma) {
+#pragma unroll
+      for (int k = 0; k < HPW; ++k)
+        if (k == tap) issue_h1(cb + 1, k);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const char* wl = wsl + (t % NS) * G::WS_B;
+    const char* hl = hal + (cb & 1) * G::HALO_B;
+    bf16x8 af[I], bfr[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(hl + h4_off(brow[j] + ky * G::HW + kx, fh));
+#pragma unroll
+    for (int i = 0; i < I; ++i) af[i] = *reinterpret_cast<const bf16x8*>(wl + h4_off(obase + i * 16 + fr, fh));
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // slab t+1 (issued at step t+1-LA) landed; the DMAs of the last LA-1 steps may stay in flight (each step
+    // issues NWI weight DMAs and, on the block's first taps, one halo DMA; counting the halo DMAs of earlier
+    // steps as landed is conservative: vmcnt retires in issue order)
+    if (hdma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail (zero-size) DMAs before the epilogue
+
+  const int hw = a.ho * a.wo;
+  float4 sc[I], bi[I];  // one sample per tile: every channel block's operands before the first store
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    sc[i] = ig_load_oscale(a, nn, o0 + obase + i * 16 + 4 * fh);
+    bi[i] = ig_load_bias(a, o0 + obase + i * 16 + 4 * fh);
+  }
+  ig_preloads_done();
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pb = pg * J + j;
+    const int oy = oy0 + pb * 16 / TW, ox = ox0 + (pb * 16) % TW + fr;
+    if (oy >= a.ho || ox >= a.wo) continue;
+    const int pix = oy * a.wo + ox;
+    const int p = nn * hw + pix;
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int ob = o0 + obase + i * 16 + 4 * fh;
+      if (ob >= a.cout_p) continue;
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
+    }
+  }
+}
+
+#define IC2_HG4_KERNEL(name, I, J, WGO, WGP, TW, NS)                                                             \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
+                                                                                          int ty) {            \
+    hg4_body<I, J, WGO, WGP, TW, NS>(a, tx, ty);                                                                 \
+  }
+IC2_HG4_KERNEL(hg4_o128_w32_kernel, 8, 4, 1, 4, 32, 3)    // 128 o x (8 x 32) px
+IC2_HG4_KERNEL(hg4_o128_w16_kernel, 8, 4, 1, 4, 16, 3)    // 128 o x (16 x 16) px
+IC2_HG4_KERNEL(hg4_o192_w32_kernel, 6, 4, 2, 2, 32, 3)    // 192 o x (4 x 32) px
+IC2_HG4_KERNEL(hg4_o192_w16_kernel, 6, 4, 2, 2, 16, 3)    // 192 o x (8 x 16) px
+IC2_HG4_KERNEL(hg4_o256_w32_kernel, 8, 4, 2, 2, 32, 3)    // 256 o x (4 x 32) px
+IC2_HG4_KERNEL(hg4_o256_w16_kernel, 8, 4, 2, 2, 16, 3)    // 256 o x (8 x 16) px
+IC2_HG4_KERNEL(hg4_o128_w32_s4_kernel, 8, 4, 1, 4, 32, 4) // 4-slab weight ring (three K-steps ahead)
+IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)
+IC2_HG4_KERNEL(hg4_o192_w32_s4_kernel, 6, 4, 2, 2, 32, 4)
+IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)
+#undef IC2_HG4_KERNEL
+
+static int hg4_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// instance: o-tile 256 when cout_p % 256 == 0, 192 when cout_p % 192 == 0, else 128 (IC2_HG4_BO=128 forces 128);
+// pixel tile 32 or 16 wide, whichever pads the output less
+struct H4Plan {
+  int bo;
+  bool tw32;
+  int64_t blocks;
+};
+static H4Plan h4_plan(int n, int ho, int wo, int cout_p) {
+  static const int force_bo = hg4_env("IC2_HG4_BO", 0);
+  H4Plan p;
+  p.bo = force_bo == 128 ? 128 : cout_p % 256 == 0 ? 256 : cout_p % 192 == 0 ? 192 : 128;
+  const int bp = p.bo == 128 ? 256 : 128;
+  const int th32 = bp / 32, th16 = bp / 16;
+  const int64_t a32 = ceil_div(ho, th32) * th32 * ceil_div(wo, 32) * 32;
+  const int64_t a16 = ceil_div(ho, th16) * th16 * ceil_div(wo, 16) * 16;
+  p.tw32 = a32 <= a16;
+  const int64_t tiles = p.tw32 ? ceil_div(ho, th32) * ceil_div(wo, 32) : ceil_div(ho, th16) * ceil_div(wo, 16);
+  p.blocks = n * tiles * ceil_div(cout_p, p.bo);
+  return p;
+}
+
+template <int I, int J, int WGO, int WGP, int TW>
+static void launch_hg4(IgemmArgs a, hipStream_t s, void (*kern)(IgemmArgs, int, int)) {
+  constexpr int BO = 16 * I * WGO, TH = 16 * J * WGP / TW;
+  const int tiles_x = (int)ceil_div(a.wo, TW), tiles_y = (int)ceil_div(a.ho, TH);
+  a.tiles_o = (a.cout_p + BO - 1) / BO;
+  a.nblocks = a.n * tiles_x * tiles_y * a.tiles_o;
+  hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(256), 0, s, a, tiles_x, tiles_y);
+}
+
+static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
+  static const int ns = hg4_env("IC2_HG4_NS", 4);  // 4-slab ring: +0.5-1 % over 3 (profiles/r2e_hg4_sweep.txt)
+  const H4Plan p = h4_plan(a.n, a.ho, a.wo, a.cout_p);
+  if (p.bo == 256) {
+    if (p.tw32) launch_hg4<8, 4, 2, 2, 32>(a, s, hg4_o256_w32_kernel);
+    else launch_hg4<8, 4, 2, 2, 16>(a, s, hg4_o256_w16_kernel);
+  } else if (p.bo == 192) {
+    if (p.tw32) launch_hg4<6, 4, 2, 2, 32>(a, s, ns == 4 ? hg4_o192_w32_s4_kernel : hg4_o192_w32_kernel);
+    else launch_hg4<6, 4, 2, 2, 16>(a, s, ns == 4 ? hg4_o192_w16_s4_kernel : hg4_o192_w16_kernel);
+  } else {
+    if (p.tw32) launch_hg4<8, 4, 1, 4, 32>(a, s, ns == 4 ? hg4_o128_w32_s4_kernel : hg4_o128_w32_kernel);
+    else launch_hg4<8, 4, 1, 4, 16>(a, s, ns == 4 ? hg4_o128_w16_s4_kernel : hg4_o128_w16_kernel);
+  }
+}
+
+// bf16 3x3 with 32-deep channel blocks.  Default: on a grid of >= 2 workgroups per CU, <= 256 channels in, <= 192
+// out, >= 93 % pixel-tile utilisation (tools/sweep_igemm.py, profiles/r2e_hg4_sweep.txt).  IC2_HG4=0 disables it, =2 forces it wherever legal (tests).
+static int hg4_mode() {
+  static const int mode = [] {
+    const char* e = getenv("IC2_HG4");
+    return e ? atoi(e) : 1;
+  }();
+  return mode;
+}
+static bool hg4_legal(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
+  if (!(dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 32 == 0 && cout_p % 64 == 0 &&
+        x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))
+    return false;
+  return true;
+}
+static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
+  const int mode = hg4_mode();
+  if (!mode || !hg4_legal(dtype, cin_p, cout_p, kh, kw, x_elems, n, ho, wo)) return false;
+  if (mode == 2) return true;
+  const H4Plan p = h4_plan(n, ho, wo, cout_p);
+  if (p.blocks < 512) return false;
+  const int th = (p.bo == 128 ? 256 : 128) / (p.tw32 ? 32 : 16);
+  const double util = (double)ho * wo / ((double)ceil_div(ho, th) * th * ceil_div(wo, p.tw32 ? 32 : 16) * (p.tw32 ? 32 : 16));
+  static const int max_cout = hg4_env("IC2_HG4_MAXC", 192);  // the 256-wide layers measured faster on hgemm
+  return cin_p <= 256 && cout_p <= max_cout && util >= 0.93;
 }
 
 static void hgemm_dispatch(const IgemmArgs& a, hipStream_t s) {
@@ -1050,6 +1371,13 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
 #pragma unroll
         for (int r = 0; r < GL; ++r) gs[i][r] = gq[i][r] = 0.f;
     }
+    float4 sc[C::OB], bi[C::OB];  // every channel block's operands before the first store (see ig_load_oscale)
+#pragma unroll
+    for (int i = 0; i < C::OB; ++i) {
+      sc[i] = ig_load_oscale(a, nn, 16 * i + 4 * fh);
+      bi[i] = ig_load_bias(a, 16 * i + 4 * fh);
+    }
+    ig_preloads_done();
 #pragma unroll
     for (int j = 0; j < C::JB; ++j) {
       const int pb = wave + 8 * j;
@@ -1060,10 +1388,9 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
 #pragma unroll
       for (int i = 0; i < C::OB; ++i) {
         const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        ig_store4(a, p, nn, pix, 16 * i + 4 * fh, v);
+        ig_store4v(a, p, nn, pix, 16 * i + 4 * fh, v, sc[i], bi[i]);
         if constexpr (GN) {  // statistics of the value as stored: bias added, rounded to bf16
-          const float4 bi = *reinterpret_cast<const float4*>(a.bias + 16 * i + 4 * fh);
-          const float bv[4] = {bi.x, bi.y, bi.z, bi.w};
+          const float bv[4] = {bi[i].x, bi[i].y, bi[i].z, bi[i].w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float st = bf2f(f2bf(v[r] + bv[r]));
@@ -1218,7 +1545,8 @@ extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int 
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
   const int64_t M = (int64_t)n * ho * wo;
-  if (hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo) &&
+  if ((hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo) ||
+       hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo)) &&
       !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw))
     return 0;
   const IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
@@ -1265,10 +1593,14 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype);
   const bool hconv = !torgb && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
-  const bool hgemm = !torgb && !hconv && hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
+  const bool hg4 = !torgb && !hconv && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
+  const bool hgemm =
+      !torgb && !hconv && (hg4 || hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo));
   if (hgemm) pl.splits = 1;
   if (torgb) {
     launch_torgb(a, s);
+  } else if (hg4) {
+    hg4_dispatch(a, s);
   } else if (hgemm) {
     hgemm_dispatch(a, s);
   } else if (hconv) {

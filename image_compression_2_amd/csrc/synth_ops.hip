@@ -79,10 +79,9 @@ __global__ void __launch_bounds__(256) upfirdn2d_kernel(const T* __restrict__ x,
 // ------------------------------------------------------------------------------------------------
 constexpr int FC_OPB = 2;
 
-__global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
-                                                 const float* __restrict__ b, float* __restrict__ y, int n, int in_f,
-                                                 int out_f, float w_gain, float b_gain, int act, float alpha,
-                                                 float act_gain, int vec) {
+__device__ __forceinline__ void fc_body(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                        const float* __restrict__ b, float* __restrict__ y, int n, int in_f, int out_f,
+                                        float w_gain, float b_gain, int act, float alpha, float act_gain, int vec) {
   const int t = threadIdx.x;
   const int r = t >> 3, sl = t & 7;
   const int nn = blockIdx.y * 32 + r;
@@ -131,6 +130,13 @@ __global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, in
       y[(int64_t)nn * out_f + o0 + o] = v;
     }
   }
+}
+
+__global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                                 const float* __restrict__ b, float* __restrict__ y, int n, int in_f,
+                                                 int out_f, float w_gain, float b_gain, int act, float alpha,
+                                                 float act_gain, int vec) {
+  fc_body(x, ldx, w, b, y, n, in_f, out_f, w_gain, b_gain, act, alpha, act_gain, vec);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -184,8 +190,8 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // xscale = s * g with g = rsqrt(mean(s^2)) over the whole batch (demod) or style_gain: one workgroup,
 // f64 sum of squares (fixed order: per-thread strided sums, wave xor-tree, then 16 wave totals in order)
-__global__ void __launch_bounds__(1024) style_xscale_kernel(const float* __restrict__ s, int n, int cin, int cin_p,
-                                                            int demod, float style_gain, float* __restrict__ xs) {
+__device__ __forceinline__ void style_xscale_body(const float* __restrict__ s, int n, int cin, int cin_p, int demod,
+                                                  float style_gain, float* __restrict__ xs) {
   __shared__ double red[16];
   __shared__ float gsh;
   const int64_t total = (int64_t)n * cin;
@@ -213,10 +219,15 @@ __global__ void __launch_bounds__(1024) style_xscale_kernel(const float* __restr
   }
 }
 
+__global__ void __launch_bounds__(1024) style_xscale_kernel(const float* __restrict__ s, int n, int cin, int cin_p,
+                                                            int demod, float style_gain, float* __restrict__ xs) {
+  style_xscale_body(s, n, cin, cin_p, demod, style_gain, xs);
+}
+
 // one wave per (n, o): lanes over cin
-__global__ void __launch_bounds__(256) oscale_kernel(const float* __restrict__ xs, const float* __restrict__ wsq,
-                                                     int n, int cin, int cin_p, int cout, int cout_p, int demod,
-                                                     float input_gain, float* __restrict__ os) {
+__device__ __forceinline__ void oscale_body(const float* __restrict__ xs, const float* __restrict__ wsq, int n, int cin,
+                                            int cin_p, int cout, int cout_p, int demod, float input_gain,
+                                            float* __restrict__ os) {
   const int lane = threadIdx.x & 63;
   const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= (int64_t)n * cout_p) return;
@@ -238,6 +249,52 @@ __global__ void __launch_bounds__(256) oscale_kernel(const float* __restrict__ x
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if (lane == 0) os[item] = input_gain * rsqrtf(acc + 1e-8f);
+}
+
+__global__ void __launch_bounds__(256) oscale_kernel(const float* __restrict__ xs, const float* __restrict__ wsq,
+                                                     int n, int cin, int cin_p, int cout, int cout_p, int demod,
+                                                     float input_gain, float* __restrict__ os) {
+  oscale_body(xs, wsq, n, cin, cin_p, cout, cout_p, demod, input_gain, os);
+}
+
+// ------------------------------------------------------------------------------------------------
+// All synthesis layers' modulation coefficients in three launches (the per-layer form above costs three
+// small launches per layer, ~0.5 ms per C2 step for 15 layers): blockIdx.z / blockIdx.x = layer, each
+// layer's arithmetic exactly the per-layer kernels' (same bodies), so the results are bit-identical.
+// ------------------------------------------------------------------------------------------------
+constexpr int kModMaxLayers = 20;
+struct ModLayer {
+  const float* aw;   // affine weight [cin][w_dim]
+  const float* ab;   // affine bias [cin]
+  const float* wsq;  // [cout][cin] (demodulated layers)
+  float* styles;     // [n][cin] scratch
+  float* xs;         // [n][cin_p]
+  float* os;         // [n][cout_p]
+  int64_t ws_off;    // element offset of this layer's w row in ws
+  int cin, cin_p, cout, cout_p, demod, vec;
+  float w_gain, b_gain, style_gain, input_gain;
+};
+struct ModBatch {
+  int nl, n, w_dim;
+  int64_t ldx;
+  const float* ws;
+  ModLayer L[kModMaxLayers];
+};
+
+__global__ void __launch_bounds__(256) fc_multi_kernel(ModBatch mb) {
+  const ModLayer& L = mb.L[blockIdx.z];
+  if ((int)blockIdx.x * FC_OPB >= L.cin) return;
+  fc_body(mb.ws + L.ws_off, mb.ldx, L.aw, L.ab, L.styles, mb.n, mb.w_dim, L.cin, L.w_gain, L.b_gain, IC2_ACT_LINEAR,
+          0.f, 1.f, L.vec);
+}
+__global__ void __launch_bounds__(1024) style_xscale_multi_kernel(ModBatch mb) {
+  const ModLayer& L = mb.L[blockIdx.x];
+  style_xscale_body(L.styles, mb.n, L.cin, L.cin_p, L.demod, L.style_gain, L.xs);
+}
+__global__ void __launch_bounds__(256) oscale_multi_kernel(ModBatch mb) {
+  const ModLayer& L = mb.L[blockIdx.y];
+  if ((int64_t)blockIdx.x * 4 >= (int64_t)mb.n * L.cout_p) return;
+  oscale_body(L.xs, L.wsq, mb.n, L.cin, L.cin_p, L.cout, L.cout_p, L.demod, L.input_gain, L.os);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -396,6 +453,44 @@ extern "C" int ic2_modconv_prep(const float* styles, const float* wsq, int n, in
   hipLaunchKernelGGL(oscale_kernel, dim3((unsigned)ceil_div((int64_t)n * cout_p, 4)), dim3(256), 0, s, xscale_out, wsq,
                      n, cin, cin_p, cout, cout_p, demod, input_gain, oscale_out);
   IC2_CHECK_LAUNCH("modconv_prep");
+  return IC2_OK;
+}
+
+// layers: nl records of 16 int64 slots each (host array): {aw, ab, wsq, styles, xs, os, ws_off, cin, cin_p, cout,
+// cout_p, demod, w_gain, b_gain, style_gain, input_gain} (pointers as integers, gains as float bit patterns in
+// the low 32 bits) -- see include/ic2ops.h.
+extern "C" int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int w_dim, int nl, const int64_t* layers,
+                                        void* stream) {
+  IC2_CHECK_ARG(ws && layers && n > 0 && w_dim > 0 && ldx >= w_dim && nl > 0 && nl <= kModMaxLayers,
+                "modconv_prep_batched: bad arguments (nl=%d, max %d)", nl, kModMaxLayers);
+  ModBatch mb;
+  mb.nl = nl; mb.n = n; mb.w_dim = w_dim; mb.ldx = ldx; mb.ws = ws;
+  int max_cin = 0;
+  int64_t max_items = 0;
+  auto f32 = [](int64_t v) { return __builtin_bit_cast(float, (uint32_t)v); };
+  for (int l = 0; l < nl; ++l) {
+    const int64_t* r = layers + 16 * l;
+    ModLayer& L = mb.L[l];
+    L.aw = reinterpret_cast<const float*>(r[0]); L.ab = reinterpret_cast<const float*>(r[1]);
+    L.wsq = reinterpret_cast<const float*>(r[2]); L.styles = reinterpret_cast<float*>(r[3]);
+    L.xs = reinterpret_cast<float*>(r[4]); L.os = reinterpret_cast<float*>(r[5]);
+    L.ws_off = r[6]; L.cin = (int)r[7]; L.cin_p = (int)r[8]; L.cout = (int)r[9]; L.cout_p = (int)r[10];
+    L.demod = (int)r[11]; L.w_gain = f32(r[12]); L.b_gain = f32(r[13]); L.style_gain = f32(r[14]);
+    L.input_gain = f32(r[15]);
+    IC2_CHECK_ARG(L.aw && L.styles && L.xs && L.os && L.cin > 0 && L.cin_p >= L.cin && L.cout > 0 &&
+                      L.cout_p >= L.cout && (!L.demod || L.wsq) && L.ws_off >= 0 && L.ws_off + w_dim <= ldx,
+                  "modconv_prep_batched: bad layer record %d", l);
+    L.vec = w_dim % 32 == 0 && ldx % 4 == 0 && L.ws_off % 4 == 0 && ((uintptr_t)ws | (uintptr_t)L.aw) % 16 == 0;
+    max_cin = max_cin > L.cin ? max_cin : L.cin;
+    const int64_t items = (int64_t)n * L.cout_p;
+    max_items = max_items > items ? max_items : items;
+  }
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(fc_multi_kernel, dim3((unsigned)ceil_div(max_cin, FC_OPB), (unsigned)ceil_div(n, 32), nl), dim3(256),
+                     0, s, mb);
+  hipLaunchKernelGGL(style_xscale_multi_kernel, dim3(nl), dim3(1024), 0, s, mb);
+  hipLaunchKernelGGL(oscale_multi_kernel, dim3((unsigned)ceil_div(max_items, 4), nl), dim3(256), 0, s, mb);
+  IC2_CHECK_LAUNCH("modconv_prep_batched");
   return IC2_OK;
 }
 

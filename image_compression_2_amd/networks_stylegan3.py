@@ -561,14 +561,40 @@ class SynthesisNetwork(torch.nn.Module):
         n = ws.shape[0]
         ldx = self.num_ws * self.w_dim
         layers = self.layers()
-        # all per-layer modulation coefficients first (each step needs the next layer's xscale)
-        flat = ws.view(-1)
-        sc = [L.scales(flat[(i + 1) * self.w_dim:], ldx, n, dt) for i, L in enumerate(layers)]
+        # all per-layer modulation coefficients first (each step needs the next layer's xscale): one batched
+        # affine FC + (de)modulation prep for every layer (three launches, bit-identical to L.scales per layer)
+        sc = self.scales_batched(ws, ldx, n, dt)
         x = self.input.run_nhwc(ws, ldx, n, dt, sc[0][0])
         for i, L in enumerate(layers):
             post = sc[i + 1][0] if i + 1 < len(layers) else None
             x = L.run_nhwc(x, n, dt, sc[i][1], post, final_scale=self.output_scale if L.is_torgb else None)
         return x
+
+    def scales_batched(self, ws, ldx, n, dt):
+        """[(xscale [n][cin_p], oscale [n][cout_p]) per layer] through ic2_modconv_prep_batched."""
+        layers = self.layers()
+        f32 = lambda v: int(np.float32(v).view(np.uint32))  # noqa: E731
+        sizes = [(n * L.in_channels + 3) // 4 * 4 + n * L.cin_p + n * L.cout_p for L in layers]
+        buf = torch.empty([sum(sizes)], dtype=torch.float32, device=ws.device)
+        rec = np.zeros([len(layers), 16], dtype=np.int64)
+        out, off = [], 0
+        for i, L in enumerate(layers):
+            _, wsq, _ = L.packed(dt)
+            ns = (n * L.in_channels + 3) // 4 * 4
+            styles = buf[off:off + ns]
+            xs = buf[off + ns:off + ns + n * L.cin_p].view(n, L.cin_p)
+            os_ = buf[off + ns + n * L.cin_p:off + sizes[i]].view(n, L.cout_p)
+            off += sizes[i]
+            fc = L.affine
+            style_gain = float(1 / np.sqrt(L.in_channels * (L.conv_kernel ** 2))) if L.is_torgb else 1.0
+            dp = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+            rec[i] = [dp(fc.weight), dp(fc.bias), dp(wsq), dp(styles), dp(xs), dp(os_),
+                      (i + 1) * self.w_dim, L.in_channels, L.cin_p, L.out_channels, L.cout_p, int(not L.is_torgb),
+                      f32(fc.weight_gain), f32(fc.bias_gain), f32(style_gain), f32(L.input_gain())]
+            out.append((xs, os_))
+        nv.call("ic2_modconv_prep_batched", nv.ptr(ws), ldx, n, self.w_dim, len(layers),
+                rec.ctypes.data_as(ctypes.c_void_p), nv.stream_of(ws))
+        return out
 
     def forward_train(self, ws, dt):
         """Autograd path w.r.t. ws (the reference's encoder training, stylegan3_hvae_full.py:669-696): input

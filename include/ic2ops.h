@@ -131,6 +131,16 @@ int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int 
                      int demod, float style_gain, float input_gain, float* xscale_out, float* oscale_out,
                      float* scratch, void* stream);
 
+/* Every synthesis layer's affine FC + ic2_modconv_prep in three launches (bit-identical to ic2_fc followed by
+ * ic2_modconv_prep per layer).  ws [n][ldx] f32 (the broadcast ws rows); layers: nl <= 20 records of 16 int64:
+ *   {aw, ab, wsq, styles, xscale_out, oscale_out, ws_off, cin, cin_p, cout, cout_p, demod,
+ *    w_gain, b_gain, style_gain, input_gain}
+ * pointers as integers (device memory; styles [n][cin] is scratch), the four gains as the float's bit pattern.
+ * Layer l's FC reads ws[row][ws_off .. ws_off + w_dim).  Replaces the per-layer affine + modulation of
+ * SynthesisLayer.forward [SG3-public] at the call site SynthesisNetwork.forward (stylegan3_hvae_full.py:274,329). */
+int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int w_dim, int nl, const int64_t* layers,
+                             void* stream);
+
 /* NHWC implicit-GEMM convolution on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32):
  *   acc[n,p,o] = sum_{ky,kx,i} w[o][ky][kx][i] * x[n, p + (ky,kx) - pad, i]   (zero outside the image)
  *   v = acc * (oscale ? oscale[n][o] : 1) + (bias ? bias[o] : 0);  if act: v = clamp(lrelu(v)*act_gain)

@@ -385,6 +385,22 @@ def test_conv_halo_gemm(cuda, cin, cout, size, pad):
     _conv_case(cin, cout, size, pad, n=8)
 
 
+@pytest.mark.parametrize("cin,cout,size,pad", [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1),
+                                              (256, 256, 30, 2), (32, 256, 29, 1), (128, 384, 20, 1), (64, 320, 21, 1),
+                                              (181, 128, 37, 2)])
+def test_conv_halo_gemm4(cuda, cin, cout, size, pad):
+    """The 4-wave halo implicit GEMM (hg4: 32-channel blocks, two workgroups per CU) forced on every instance
+    (IC2_HG4=2, read once per process, so in a child process): 128 / 192 / 256 output channels per workgroup,
+    8 x 32 / 16 x 16 / 4 x 32 / 8 x 16 pixel tiles, cin_p a multiple of 32 but not of 64 (96, 192 -> 192),
+    partial o-tiles (320 = 2.5 x 128), ragged tile edges, pad 1 and 2 -- against F.conv2d in fp64."""
+    import subprocess, sys
+    code = (f"import sys; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
+            f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},n=4)")
+    env = dict(__import__('os').environ, IC2_HG4="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("cin_p,n,size,pad", [(32, 2, 67, 0), (64, 1, 40, 0), (128, 3, 33, 0), (64, 2, 21, 1)])
 def test_torgb_1x1_nchw(cuda, cin_p, n, size, pad):
     """ToRGB (1x1 conv to 3 channels, bf16 NHWC in, NCHW f32 out with per-sample oscale, bias, clamp and

@@ -51,6 +51,22 @@ def test_synthesis_layer_api_matches_oracle(cuda, gen256):
         assert _maxdiff(y, r) < 1e-4 * (1 + r.abs().max().item()), L["name"]
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_modconv_prep_batched_equals_per_layer(cuda, gen256, dt):
+    """ic2_modconv_prep_batched (every layer's affine FC + (de)modulation in three launches, the forward's
+    path) is bit-identical to ic2_fc + ic2_modconv_prep per layer (SynthesisLayer.scales), ToRGB included."""
+    syn = gen256.synthesis
+    n = 5
+    ws = (torch.randn(n, syn.num_ws, syn.w_dim, generator=torch.Generator().manual_seed(4)) * 1.5).to(cuda)
+    ldx = syn.num_ws * syn.w_dim
+    got = syn.scales_batched(ws, ldx, n, dt)
+    flat = ws.view(-1)
+    for i, L in enumerate(syn.layers()):
+        xs, os_ = L.scales(flat[(i + 1) * syn.w_dim:], ldx, n, dt)
+        assert torch.equal(got[i][0], xs), (L.name if hasattr(L, "name") else i, "xscale")
+        assert torch.equal(got[i][1], os_), (i, "oscale")
+
+
 def test_synthesis_input_matches_oracle(cuda, gen256):
     sd = _sd_cpu(gen256)
     inp, _ = sg3.layer_table(256)

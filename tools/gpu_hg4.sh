@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
-  -k "halo_gemm or conv_igemm" > gpurun_out/pytest_hg4.log 2>&1
+  -k "halo_gemm or conv_igemm or modconv_prep_batched or layer_api or synthesis_fp32_within" > gpurun_out/pytest_hg4.log 2>&1
 rc=$?
 tail -3 gpurun_out/pytest_hg4.log
 [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/pytest_hg4.log | head -20; exit $rc; }

@@ -16,7 +16,7 @@ from sweep_igemm import SHAPES  # noqa: E402
 
 
 def is_conv(name):
-    return ("igemm" in name or "hgemm" in name or "hconv" in name or "torgb" in name) and "splitk" not in name
+    return ("igemm" in name or "hgemm" in name or "hg4" in name or "hconv" in name or "torgb" in name) and "splitk" not in name
 
 
 def main():
