@@ -1371,13 +1371,19 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
 #pragma unroll
         for (int r = 0; r < GL; ++r) gs[i][r] = gq[i][r] = 0.f;
     }
-    float4 sc[C::OB], bi[C::OB];  // every channel block's operands before the first store (see ig_load_oscale)
+    // every channel block's operands before the first store (see ig_load_oscale); not in the 32 -> 64 instance,
+    // whose 4-waves-per-SIMD register budget (128) would spill them (measured 142 -> 179 us on e0a) and whose
+    // occupancy hides the per-block loads instead
+    constexpr bool kPre = !(CINP == 32 && COUTP == 64);
+    float4 sc[C::OB], bi[C::OB];
+    if constexpr (kPre) {
 #pragma unroll
-    for (int i = 0; i < C::OB; ++i) {
-      sc[i] = ig_load_oscale(a, nn, 16 * i + 4 * fh);
-      bi[i] = ig_load_bias(a, 16 * i + 4 * fh);
+      for (int i = 0; i < C::OB; ++i) {
+        sc[i] = ig_load_oscale(a, nn, 16 * i + 4 * fh);
+        bi[i] = ig_load_bias(a, 16 * i + 4 * fh);
+      }
+      ig_preloads_done();
     }
-    ig_preloads_done();
 #pragma unroll
     for (int j = 0; j < C::JB; ++j) {
       const int pb = wave + 8 * j;
@@ -1388,6 +1394,10 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
 #pragma unroll
       for (int i = 0; i < C::OB; ++i) {
         const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (!kPre) {
+          sc[i] = ig_load_oscale(a, nn, 16 * i + 4 * fh);
+          bi[i] = ig_load_bias(a, 16 * i + 4 * fh);
+        }
         ig_store4v(a, p, nn, pix, 16 * i + 4 * fh, v, sc[i], bi[i]);
         if constexpr (GN) {  // statistics of the value as stored: bias added, rounded to bf16
           const float bv[4] = {bi[i].x, bi[i].y, bi[i].z, bi[i].w};

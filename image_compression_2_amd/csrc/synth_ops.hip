@@ -281,11 +281,53 @@ struct ModBatch {
   ModLayer L[kModMaxLayers];
 };
 
+// Both per-layer products of the modulation are small GEMMs over <= 512-long rows:
+//   styles[n][o] = (sum_i ws[n][off + i] * aw[o][i]) * w_gain + ab[o] * b_gain      (affine FC)
+//   oscale[n][o] = input_gain * rsqrt(sum_i xs[n][i]^2 * wsq[o][i] + 1e-8)           (demodulation)
+// A workgroup owns 16 output features of one layer: their weight rows are staged in LDS once (row pitch K+1:
+// the 16 rows land in distinct banks), then 16-sample chunks of the left operand; thread (o = t & 15,
+// n = t >> 4) sums its dot product sequentially over i (fixed order, deterministic).  Replaces one wave per
+// (n, o) reading the [cout][cin] weight again for every sample (86 us per C2 step for 15 layers).
+constexpr int kSmK = 512;  // longest row (w_dim, cin)
+template <bool OSCALE>
+__device__ __forceinline__ void small_mm_body(const float* __restrict__ a, int64_t lda, const float* __restrict__ w,
+                                              int n, int K, int nout, int out_p, float* __restrict__ out,
+                                              const ModLayer& L) {
+  __shared__ float wl[16][kSmK + 1];
+  __shared__ float al[16][kSmK + 1];
+  const int t = threadIdx.x;
+  const int o0 = blockIdx.x * 16;
+  for (int e = t; e < 16 * K; e += 256) {
+    const int r = e / K, i = e - (e / K) * K;
+    wl[r][i] = o0 + r < nout ? w[(int64_t)(o0 + r) * K + i] : 0.f;
+  }
+  const int ol = t & 15, nl = t >> 4;
+  const int o = o0 + ol;
+  for (int n0 = 0; n0 < n; n0 += 16) {
+    __syncthreads();  // weights staged / previous chunk consumed
+    for (int e = t; e < 16 * K; e += 256) {
+      const int r = e / K, i = e - (e / K) * K;
+      float v = n0 + r < n ? a[(int64_t)(n0 + r) * lda + i] : 0.f;
+      if (OSCALE) v = v * v;
+      al[r][i] = v;
+    }
+    __syncthreads();
+    float acc = 0.f;
+    for (int i = 0; i < K; ++i) acc = fmaf(al[nl][i], wl[ol][i], acc);
+    const int nn = n0 + nl;
+    if (nn < n && o < out_p) {
+      float v;
+      if (OSCALE) v = o < nout ? (L.demod ? L.input_gain * rsqrtf(acc + 1e-8f) : L.input_gain) : 0.f;
+      else v = acc * L.w_gain + (L.ab ? L.ab[o] * L.b_gain : 0.f);
+      if (OSCALE || o < nout) out[(int64_t)nn * out_p + o] = v;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) fc_multi_kernel(ModBatch mb) {
-  const ModLayer& L = mb.L[blockIdx.z];
-  if ((int)blockIdx.x * FC_OPB >= L.cin) return;
-  fc_body(mb.ws + L.ws_off, mb.ldx, L.aw, L.ab, L.styles, mb.n, mb.w_dim, L.cin, L.w_gain, L.b_gain, IC2_ACT_LINEAR,
-          0.f, 1.f, L.vec);
+  const ModLayer& L = mb.L[blockIdx.y];
+  if ((int)blockIdx.x * 16 >= L.cin) return;
+  small_mm_body<false>(mb.ws + L.ws_off, mb.ldx, L.aw, mb.n, mb.w_dim, L.cin, L.cin, L.styles, L);
 }
 __global__ void __launch_bounds__(1024) style_xscale_multi_kernel(ModBatch mb) {
   const ModLayer& L = mb.L[blockIdx.x];
@@ -293,8 +335,16 @@ __global__ void __launch_bounds__(1024) style_xscale_multi_kernel(ModBatch mb) {
 }
 __global__ void __launch_bounds__(256) oscale_multi_kernel(ModBatch mb) {
   const ModLayer& L = mb.L[blockIdx.y];
-  if ((int64_t)blockIdx.x * 4 >= (int64_t)mb.n * L.cout_p) return;
-  oscale_body(L.xs, L.wsq, mb.n, L.cin, L.cin_p, L.cout, L.cout_p, L.demod, L.input_gain, L.os);
+  if ((int)blockIdx.x * 16 >= L.cout_p) return;
+  if (!L.demod) {  // oscale = input_gain on the valid channels
+    const int o0 = blockIdx.x * 16;
+    for (int e = threadIdx.x; e < mb.n * 16; e += 256) {
+      const int nn = e >> 4, o = o0 + (e & 15);
+      if (o < L.cout_p) L.os[(int64_t)nn * L.cout_p + o] = o < L.cout ? L.input_gain : 0.f;
+    }
+    return;
+  }
+  small_mm_body<true>(L.xs, L.cin_p, L.wsq, mb.n, L.cin, L.cout, L.cout_p, L.os, L);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -465,8 +515,7 @@ extern "C" int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int
                 "modconv_prep_batched: bad arguments (nl=%d, max %d)", nl, kModMaxLayers);
   ModBatch mb;
   mb.nl = nl; mb.n = n; mb.w_dim = w_dim; mb.ldx = ldx; mb.ws = ws;
-  int max_cin = 0;
-  int64_t max_items = 0;
+  int max_cin = 0, max_cout_p = 0;
   auto f32 = [](int64_t v) { return __builtin_bit_cast(float, (uint32_t)v); };
   for (int l = 0; l < nl; ++l) {
     const int64_t* r = layers + 16 * l;
@@ -481,15 +530,14 @@ extern "C" int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int
                       L.cout_p >= L.cout && (!L.demod || L.wsq) && L.ws_off >= 0 && L.ws_off + w_dim <= ldx,
                   "modconv_prep_batched: bad layer record %d", l);
     L.vec = w_dim % 32 == 0 && ldx % 4 == 0 && L.ws_off % 4 == 0 && ((uintptr_t)ws | (uintptr_t)L.aw) % 16 == 0;
+    IC2_CHECK_ARG(L.cin <= kSmK && w_dim <= kSmK, "modconv_prep_batched: rows longer than %d (layer %d)", kSmK, l);
     max_cin = max_cin > L.cin ? max_cin : L.cin;
-    const int64_t items = (int64_t)n * L.cout_p;
-    max_items = max_items > items ? max_items : items;
+    max_cout_p = max_cout_p > L.cout_p ? max_cout_p : L.cout_p;
   }
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(fc_multi_kernel, dim3((unsigned)ceil_div(max_cin, FC_OPB), (unsigned)ceil_div(n, 32), nl), dim3(256),
-                     0, s, mb);
+  hipLaunchKernelGGL(fc_multi_kernel, dim3((unsigned)ceil_div(max_cin, 16), nl), dim3(256), 0, s, mb);
   hipLaunchKernelGGL(style_xscale_multi_kernel, dim3(nl), dim3(1024), 0, s, mb);
-  hipLaunchKernelGGL(oscale_multi_kernel, dim3((unsigned)ceil_div(max_items, 4), nl), dim3(256), 0, s, mb);
+  hipLaunchKernelGGL(oscale_multi_kernel, dim3((unsigned)ceil_div(max_cout_p, 16), nl), dim3(256), 0, s, mb);
   IC2_CHECK_LAUNCH("modconv_prep_batched");
   return IC2_OK;
 }

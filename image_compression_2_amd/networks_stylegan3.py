@@ -321,18 +321,27 @@ class SynthesisLayer(torch.nn.Module):
         self._cache[dt] = (key, val)
         return val
 
-    def scales(self, ws, ldx, n, dt):
-        """Runs the affine FC and the (de)modulation prep: -> (xscale [n][cin_p], oscale [n][cout_p])."""
-        dev = ws.device
-        styles = self.affine.run(ws, ldx=ldx, n=n)
+    def mod_record(self, dt, ws_off, styles, xs, os_):
+        """This layer's ic2_modconv_prep_batched record (16 int64, see include/ic2ops.h)."""
         _, wsq, _ = self.packed(dt)
+        fc = self.affine
+        style_gain = float(1 / np.sqrt(self.in_channels * (self.conv_kernel ** 2))) if self.is_torgb else 1.0
+        f32 = lambda v: int(np.float32(v).view(np.uint32))  # noqa: E731
+        dp = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        return [dp(fc.weight), dp(fc.bias), dp(wsq), dp(styles), dp(xs), dp(os_), ws_off, self.in_channels, self.cin_p,
+                self.out_channels, self.cout_p, int(not self.is_torgb), f32(fc.weight_gain), f32(fc.bias_gain),
+                f32(style_gain), f32(self.input_gain())]
+
+    def scales(self, ws, ldx, n, dt):
+        """Runs the affine FC and the (de)modulation prep: -> (xscale [n][cin_p], oscale [n][cout_p]).
+        The same kernels as SynthesisNetwork.scales_batched (a one-layer batch), so both give identical bits."""
+        dev = ws.device
+        styles = torch.empty([n, self.in_channels], dtype=torch.float32, device=dev)
         xs = torch.empty([n, self.cin_p], dtype=torch.float32, device=dev)
         os_ = torch.empty([n, self.cout_p], dtype=torch.float32, device=dev)
-        scratch = torch.empty([4], dtype=torch.float32, device=dev)
-        style_gain = float(1 / np.sqrt(self.in_channels * (self.conv_kernel ** 2))) if self.is_torgb else 1.0
-        nv.call("ic2_modconv_prep", nv.ptr(styles), nv.ptr(wsq), n, self.in_channels, self.out_channels, self.cin_p,
-                self.cout_p, int(not self.is_torgb), style_gain, self.input_gain(), nv.ptr(xs), nv.ptr(os_),
-                nv.ptr(scratch), nv.stream_of(ws))
+        rec = np.asarray([self.mod_record(dt, 0, styles, xs, os_)], dtype=np.int64)
+        nv.call("ic2_modconv_prep_batched", nv.ptr(ws), ldx, n, self.affine.in_features, 1,
+                rec.ctypes.data_as(ctypes.c_void_p), nv.stream_of(ws))
         return xs, os_
 
     # ---- NHWC pipeline step ------------------------------------------------------------------
@@ -573,24 +582,17 @@ class SynthesisNetwork(torch.nn.Module):
     def scales_batched(self, ws, ldx, n, dt):
         """[(xscale [n][cin_p], oscale [n][cout_p]) per layer] through ic2_modconv_prep_batched."""
         layers = self.layers()
-        f32 = lambda v: int(np.float32(v).view(np.uint32))  # noqa: E731
         sizes = [(n * L.in_channels + 3) // 4 * 4 + n * L.cin_p + n * L.cout_p for L in layers]
         buf = torch.empty([sum(sizes)], dtype=torch.float32, device=ws.device)
         rec = np.zeros([len(layers), 16], dtype=np.int64)
         out, off = [], 0
         for i, L in enumerate(layers):
-            _, wsq, _ = L.packed(dt)
             ns = (n * L.in_channels + 3) // 4 * 4
             styles = buf[off:off + ns]
             xs = buf[off + ns:off + ns + n * L.cin_p].view(n, L.cin_p)
             os_ = buf[off + ns + n * L.cin_p:off + sizes[i]].view(n, L.cout_p)
             off += sizes[i]
-            fc = L.affine
-            style_gain = float(1 / np.sqrt(L.in_channels * (L.conv_kernel ** 2))) if L.is_torgb else 1.0
-            dp = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-            rec[i] = [dp(fc.weight), dp(fc.bias), dp(wsq), dp(styles), dp(xs), dp(os_),
-                      (i + 1) * self.w_dim, L.in_channels, L.cin_p, L.out_channels, L.cout_p, int(not L.is_torgb),
-                      f32(fc.weight_gain), f32(fc.bias_gain), f32(style_gain), f32(L.input_gain())]
+            rec[i] = L.mod_record(dt, (i + 1) * self.w_dim, styles, xs, os_)
             out.append((xs, os_))
         nv.call("ic2_modconv_prep_batched", nv.ptr(ws), ldx, n, self.w_dim, len(layers),
                 rec.ctypes.data_as(ctypes.c_void_p), nv.stream_of(ws))
