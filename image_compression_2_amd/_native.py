@@ -50,6 +50,7 @@ _SIGS = {
                           _I, _P, _I64, _P],
     "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "ic2_from_rgb_conv": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "ic2_nhwc_to_nchw": [_P, _I, _P, _I, _I, _I, _I, _I, _P],
     "ic2_group_norm_stats_floats": [_I, _I, _I],
     "ic2_group_norm_stats": [_P, _I, _I, _I, _I, _I, _I, _F, _P, _P],

@@ -452,6 +452,99 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
   return IC2_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// from_rgb straight from the NCHW f32 image (HVAE_VGG_Encoder.from_rgb, stylegan3_hvae_full.py:62,175):
+// 3x3, pad 1, cin <= 4, bias, bf16 NHWC [n][h][w][COUT] out.  The MFMA path first packs the image to a
+// 32-channel bf16 NHWC tensor (10x the bytes of the 3-channel image) and then reads it back; here a workgroup
+// stages its (8+2) x (32+2) x cin input tile in LDS (rounded to bf16 exactly as that packing does) and each
+// thread computes one pixel's COUT outputs with packed FMAs against the bf16 weights held in LDS (broadcast
+// reads).  Arithmetic: bf16 operands, f32 sums (tap order), + bias, one bf16 rounding -- as the MFMA conv.
+// ------------------------------------------------------------------------------------------------
+template <int COUT>
+__global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const bf16_t* __restrict__ wp,
+                                                       int cin_p, const float* __restrict__ bias, bf16_t* __restrict__ y,
+                                                       int h, int w, int tiles_x, int tiles_y) {
+  constexpr int TH = 8, TW = 32, HH = TH + 2, HW = TW + 2;
+  __shared__ float xin[4][HH][HW + 1];
+  __shared__ __attribute__((aligned(16))) float wl[36][COUT];  // [tap * cin + c][o]
+  const int t = threadIdx.x;
+  int b = blockIdx.x;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int nn = b / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int nk = 9 * cin;
+  for (int e = t; e < nk * COUT; e += 256) {
+    const int o = e % COUT, k = e / COUT;
+    const int tap = k / cin, c = k - (k / cin) * cin;
+    wl[k][o] = bf2f(wp[((int64_t)o * 9 + tap) * cin_p + c]);
+  }
+  for (int e = t; e < cin * HH * HW; e += 256) {
+    const int c = e / (HH * HW), r = e - c * (HH * HW);
+    const int yy = r / HW, xx = r - (r / HW) * HW;
+    const int iy = oy0 - 1 + yy, ix = ox0 - 1 + xx;
+    float v = 0.f;
+    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) v = bf2f(f2bf(x[(((int64_t)nn * cin + c) * h + iy) * w + ix]));
+    xin[c][yy][xx] = v;
+  }
+  __syncthreads();
+  const int py = t >> 5, px = t & 31;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 acc[COUT / 2];
+#pragma unroll
+  for (int o = 0; o < COUT / 2; ++o) acc[o] = f2{0.f, 0.f};
+  for (int tap = 0; tap < 9; ++tap) {
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    for (int c = 0; c < cin; ++c) {
+      const float xv = xin[c][py + ky][px + kx];
+      const f2 xx = f2{xv, xv};
+      const float4* wr = reinterpret_cast<const float4*>(&wl[tap * cin + c][0]);
+#pragma unroll
+      for (int q = 0; q < COUT / 4; ++q) {
+        const float4 wv = wr[q];
+        acc[2 * q] = __builtin_elementwise_fma(xx, f2{wv.x, wv.y}, acc[2 * q]);
+        acc[2 * q + 1] = __builtin_elementwise_fma(xx, f2{wv.z, wv.w}, acc[2 * q + 1]);
+      }
+    }
+  }
+  const int oy = oy0 + py, ox = ox0 + px;
+  if (oy >= h || ox >= w) return;
+  bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * COUT;
+#pragma unroll
+  for (int q = 0; q < COUT / 8; ++q) {
+    uint4 pk;
+    uint32_t u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = 8 * q + 2 * k;
+      u[k] = (uint32_t)f2bf(acc[o / 2].x + bias[o]) | ((uint32_t)f2bf(acc[o / 2].y + bias[o + 1]) << 16);
+    }
+    pk.x = u[0]; pk.y = u[1]; pk.z = u[2]; pk.w = u[3];
+    reinterpret_cast<uint4*>(yo)[q] = pk;
+  }
+}
+
+extern "C" int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin_p, const float* bias, void* y, int n,
+                                 int h, int w_, int cout_p, void* stream) {
+  IC2_CHECK_ARG(x && w && bias && y && n > 0 && h > 0 && w_ > 0, "from_rgb_conv: null pointer / bad geometry");
+  IC2_CHECK_ARG(cin >= 1 && cin <= 4 && cin_p >= cin && (cout_p == 32 || cout_p == 64),
+                "from_rgb_conv: needs 1 <= cin <= 4 and cout_p in {32, 64} (cin=%d cout_p=%d)", cin, cout_p);
+  IC2_CHECK_ARG((uintptr_t)y % 16 == 0, "from_rgb_conv: output must be 16-byte aligned");
+  const int tiles_x = (w_ + 31) / 32, tiles_y = (h + 7) / 8;
+  const int64_t blocks = (int64_t)n * tiles_x * tiles_y;
+  IC2_CHECK_ARG(blocks < (1LL << 31), "from_rgb_conv: too many tiles");
+  hipStream_t s = as_stream(stream);
+  if (cout_p == 32)
+    hipLaunchKernelGGL(from_rgb_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, (const bf16_t*)w, cin_p, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL(from_rgb_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, (const bf16_t*)w, cin_p, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  IC2_CHECK_LAUNCH("from_rgb_conv");
+  return IC2_OK;
+}
+
 extern "C" int ic2_nhwc_to_nchw(const void* x, int dtype, float* y, int n, int c, int h, int w, int c_p, void* stream) {
   IC2_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && c_p >= c, "nhwc_to_nchw: bad arguments");
   const int64_t total = (int64_t)n * h * w * c;

@@ -1097,6 +1097,8 @@ IC2_HG4_KERNEL(hg4_o128_w32_s4_kernel, 8, 4, 1, 4, 32, 4) // 4-slab weight ring 
 IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)
 IC2_HG4_KERNEL(hg4_o192_w32_s4_kernel, 6, 4, 2, 2, 32, 4)
 IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)
+IC2_HG4_KERNEL(hg4_o64_w32_s4_kernel, 4, 4, 1, 4, 32, 4)   // 64 o x (8 x 32) px: the 64-wide layers
+IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)
 #undef IC2_HG4_KERNEL
 
 static int hg4_env(const char* name, int dflt) {
@@ -1114,8 +1116,8 @@ struct H4Plan {
 static H4Plan h4_plan(int n, int ho, int wo, int cout_p) {
   static const int force_bo = hg4_env("IC2_HG4_BO", 0);
   H4Plan p;
-  p.bo = force_bo == 128 ? 128 : cout_p % 256 == 0 ? 256 : cout_p % 192 == 0 ? 192 : 128;
-  const int bp = p.bo == 128 ? 256 : 128;
+  p.bo = force_bo == 128 ? 128 : cout_p % 256 == 0 ? 256 : cout_p % 192 == 0 ? 192 : cout_p % 128 == 0 ? 128 : 64;
+  const int bp = p.bo <= 128 ? 256 : 128;
   const int th32 = bp / 32, th16 = bp / 16;
   const int64_t a32 = ceil_div(ho, th32) * th32 * ceil_div(wo, 32) * 32;
   const int64_t a16 = ceil_div(ho, th16) * th16 * ceil_div(wo, 16) * 16;
@@ -1143,9 +1145,12 @@ static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
   } else if (p.bo == 192) {
     if (p.tw32) launch_hg4<6, 4, 2, 2, 32>(a, s, ns == 4 ? hg4_o192_w32_s4_kernel : hg4_o192_w32_kernel);
     else launch_hg4<6, 4, 2, 2, 16>(a, s, ns == 4 ? hg4_o192_w16_s4_kernel : hg4_o192_w16_kernel);
-  } else {
+  } else if (p.bo == 128) {
     if (p.tw32) launch_hg4<8, 4, 1, 4, 32>(a, s, ns == 4 ? hg4_o128_w32_s4_kernel : hg4_o128_w32_kernel);
     else launch_hg4<8, 4, 1, 4, 16>(a, s, ns == 4 ? hg4_o128_w16_s4_kernel : hg4_o128_w16_kernel);
+  } else {
+    if (p.tw32) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_s4_kernel);
+    else launch_hg4<4, 4, 1, 4, 16>(a, s, hg4_o64_w16_s4_kernel);
   }
 }
 
@@ -1170,7 +1175,7 @@ static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64
   if (mode == 2) return true;
   const H4Plan p = h4_plan(n, ho, wo, cout_p);
   if (p.blocks < 512) return false;
-  const int th = (p.bo == 128 ? 256 : 128) / (p.tw32 ? 32 : 16);
+  const int th = (p.bo <= 128 ? 256 : 128) / (p.tw32 ? 32 : 16);
   const double util = (double)ho * wo / ((double)ceil_div(ho, th) * th * ceil_div(wo, p.tw32 ? 32 : 16) * (p.tw32 ? 32 : 16));
   static const int max_cout = hg4_env("IC2_HG4_MAXC", 192);  // the 256-wide layers measured faster on hgemm
   return cin_p <= 256 && cout_p <= max_cout && util >= 0.93;
@@ -1602,8 +1607,14 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype);
-  const bool hconv = !torgb && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
-  const bool hg4 = !torgb && !hconv && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
+  // hg4 ahead of the halo direct conv: for 96 input channels (SG3-T-1024 L11: 1532 -> 1363 us at batch 8); the
+  // 32 / 64-channel encoder layers stay on hconv (faster there).  IC2_HG4_HCONV=0 / 1: never / always.
+  static const int hg4_over_hconv = hg4_env("IC2_HG4_HCONV", -1);
+  const bool hg4_pref = hg4_over_hconv == 1 || (hg4_over_hconv < 0 && cin_p >= 96);
+  const bool hg4_first = hg4_pref && !torgb && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
+  const bool hconv = !torgb && !hg4_first && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
+  const bool hg4 = hg4_first ||
+                   (!torgb && !hconv && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo));
   const bool hgemm =
       !torgb && !hconv && (hg4 || hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo));
   if (hgemm) pl.splits = 1;

@@ -17,6 +17,9 @@ opt-in extension.
 """
 from __future__ import annotations
 
+import os
+import types
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -73,6 +76,26 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
                   x.c_p, cout_p, cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream,
                   x.t.device)
     return _Act(y, cout)
+
+
+# IC2_FROM_RGB_DIRECT=0 keeps the packing + implicit-GEMM from_rgb (A/B switch)
+_FROM_RGB_DIRECT = os.environ.get("IC2_FROM_RGB_DIRECT", "1") != "0"
+
+
+def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream):
+    """from_rgb on the NCHW f32 image: in bf16 mode one direct kernel (ic2_from_rgb_conv: no 32-channel packed copy
+    of the image), else the packing + implicit GEMM."""
+    cout, cin, kh, kw = conv.weight.shape
+    if (dt == torch.bfloat16 and cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1
+            and nv.pad32(cout) in (32, 64) and _FROM_RGB_DIRECT):
+        n, _, hh, ww = x.shape
+        fake = types.SimpleNamespace(c=cin, c_p=nv.pad32(cin))
+        wp, bp = _packed(conv, fake, dt, cache, stream)
+        y = torch.empty([n, hh, ww, wp.shape[0]], dtype=dt, device=x.device)
+        nv.call("ic2_from_rgb_conv", nv.ptr(x), cin, nv.ptr(wp), fake.c_p, nv.ptr(bp), nv.ptr(y), n, hh, ww,
+                wp.shape[0], stream)
+        return _Act(y, cout)
+    return _conv(conv, _to_nhwc(x, dt, stream), dt, cache, stream)
 
 
 def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stream, fuse=-1):
@@ -186,8 +209,7 @@ class HVAE_VGG_Encoder(nn.Module):
 
     def features_nhwc(self, x, dt, stream):
         """from_rgb + blocks with the reference's 1x1 break; returns {'fine','medium','global'} -> _Act."""
-        h = _to_nhwc(x, dt, stream)
-        h = _conv(self.from_rgb, h, dt, self._cache, stream)
+        h = _from_rgb(self.from_rgb, x, dt, self._cache, stream)
         feats = {}
         for i, block in enumerate(self.blocks):
             if h.h <= 1 or h.w <= 1:

@@ -175,6 +175,13 @@ int ic2_synth_input_features(const float* t, const float* freqs, const float* ph
 
 /* NCHW f32 -> NHWC (dtype) with channel stride c_p (zero padded), optionally times scale[n][c_p]
  * (nullable; a modulated layer's input scaling); the encoder's input packing. */
+/* HVAE_VGG_Encoder.from_rgb (nn.Conv2d(cin, cout, 3, padding=1), stylegan3_hvae_full.py:62,175) read straight
+ * from the NCHW f32 image: x [n][cin][h][w] f32 (cin <= 4, rounded to bf16 as ic2_nchw_to_nhwc does), w packed
+ * bf16 [cout_p][3][3][cin_p] (ic2_pack_weight), bias [cout_p] f32 -> y bf16 NHWC [n][h][w][cout_p], cout_p in
+ * {32, 64}.  Equals ic2_nchw_to_nhwc + ic2_conv_igemm (bf16) up to f32 summation order. */
+int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin_p, const float* bias, void* y, int n, int h,
+                      int w_, int cout_p, void* stream);
+
 int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c, int h, int w, int c_p, const float* scale,
                      void* stream);
 

@@ -387,10 +387,10 @@ def test_conv_halo_gemm(cuda, cin, cout, size, pad):
 
 @pytest.mark.parametrize("cin,cout,size,pad", [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1),
                                               (256, 256, 30, 2), (32, 256, 29, 1), (128, 384, 20, 1), (64, 320, 21, 1),
-                                              (181, 128, 37, 2)])
+                                              (181, 128, 37, 2), (81, 51, 37, 2), (64, 64, 33, 1)])
 def test_conv_halo_gemm4(cuda, cin, cout, size, pad):
     """The 4-wave halo implicit GEMM (hg4: 32-channel blocks, two workgroups per CU) forced on every instance
-    (IC2_HG4=2, read once per process, so in a child process): 128 / 192 / 256 output channels per workgroup,
+    (IC2_HG4=2, read once per process, so in a child process): 64 / 128 / 192 / 256 output channels per workgroup,
     8 x 32 / 16 x 16 / 4 x 32 / 8 x 16 pixel tiles, cin_p a multiple of 32 but not of 64 (96, 192 -> 192),
     partial o-tiles (320 = 2.5 x 128), ragged tile edges, pad 1 and 2 -- against F.conv2d in fp64."""
     import subprocess, sys
@@ -399,6 +399,32 @@ def test_conv_halo_gemm4(cuda, cin, cout, size, pad):
     env = dict(__import__('os').environ, IC2_HG4="2")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(3, 32, 3, 67, 45), (3, 64, 2, 40, 33), (1, 32, 1, 9, 70), (4, 32, 2, 16, 32)])
+def test_from_rgb_direct(cuda, cin, cout, n, h, w):
+    """ic2_from_rgb_conv (from_rgb read straight from the NCHW f32 image, bf16 NHWC out) against F.conv2d in fp64
+    on the same bf16-rounded operands, and against the packing + implicit-GEMM path it replaces (they differ
+    only by f32 summation order: at most one bf16 rounding step apart)."""
+    g = torch.Generator().manual_seed(cin * 100 + cout)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    x = torch.rand(n, cin, h, w, generator=g) * 2 - 1
+    convg, xd = conv.to(cuda), x.to(cuda)
+    stream = nv.stream_of(xd)
+    from image_compression_2_amd import stylegan3_hvae_full as shf
+    y = shf._from_rgb(convg, xd, torch.bfloat16, {}, stream)
+    y_ref_path = shf._conv(convg, shf._to_nhwc(xd, torch.bfloat16, stream), torch.bfloat16, {}, stream)
+    torch.cuda.synchronize()
+    a = y.t[..., :cout].float().cpu().permute(0, 3, 1, 2)
+    b = y_ref_path.t[..., :cout].float().cpu().permute(0, 3, 1, 2)
+    r = F.conv2d(x.to(torch.bfloat16).double(), conv.weight.detach().cpu().to(torch.bfloat16).double(),
+                 conv.bias.detach().cpu().double(), padding=1)
+    assert (a.double() - r).abs().max().item() < 1e-2 * (1 + r.abs().max().item())
+    assert (a - b).abs().max().item() <= 2 ** -7 * (1 + b.abs().max().item())
+    assert torch.equal(y.t[..., cout:].cpu(), torch.zeros_like(y.t[..., cout:].cpu()))
 
 
 @pytest.mark.parametrize("cin_p,n,size,pad", [(32, 2, 67, 0), (64, 1, 40, 0), (128, 3, 33, 0), (64, 2, 21, 1)])

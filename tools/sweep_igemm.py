@@ -20,18 +20,24 @@ SHAPES = [("e_rgb", 3, 32, 256, 1), ("e0a", 32, 64, 256, 1), ("e0b", 64, 64, 256
           ("s36", 512, 512, 36, 2), ("s52", 512, 512, 52, 2), ("s84", 512, 512, 84, 2), ("s148", 512, 512, 148, 2),
           ("s148b", 512, 362, 148, 2), ("s148c", 362, 256, 148, 2), ("s276a", 256, 181, 276, 2),
           ("s276b", 181, 128, 276, 2), ("s276c", 128, 128, 276, 2)]
+# SWEEP_SET=c4: the C4 workload's (batch 8) high-resolution shapes: encoder at 1024^2 / 512^2, SG3-T-1024 L8-L13
+SHAPES_C4 = [("E_rgb", 3, 32, 1024, 1), ("E0a", 32, 64, 1024, 1), ("E0b", 64, 64, 1024, 1), ("E1a", 64, 128, 512, 1),
+             ("E1b", 128, 128, 512, 1), ("T8", 323, 203, 276, 2), ("T9", 203, 128, 276, 2), ("T10", 128, 81, 532, 2),
+             ("T11", 81, 51, 1044, 2), ("T12", 51, 32, 1044, 2), ("T13", 32, 32, 1044, 2)]
+if os.environ.get("SWEEP_SET") == "c4":
+    SHAPES = SHAPES_C4
 
 
 def child(only):
     import torch
     from image_compression_2_amd import _native as nv
     dev = torch.device("cuda", 0)
-    n = 32
+    n = 8 if os.environ.get("SWEEP_SET") == "c4" else 32
     res = {}
     for name, ci, co, s, pad in SHAPES:
         if only and name not in only:
             continue
-        cip, cop = nv.pad32(ci), nv.pad32(co)
+        cip, cop = (nv.pad_synth(ci), nv.pad_synth(co)) if name[0] in "sT" else (nv.pad32(ci), nv.pad32(co))
         ho = s + 2 * pad - 2
         x = torch.randn(n, s, s, cip, device=dev).to(torch.bfloat16)
         w = (torch.randn(cop, 3, 3, cip, device=dev) / (9 * cip) ** 0.5).to(torch.bfloat16)
