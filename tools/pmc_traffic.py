@@ -26,7 +26,7 @@ def main():
         for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"]
-                if not any(t in k for t in ("igemm", "hconv_kernel", "torgb_kernel")):
+                if not any(t in k for t in ("igemm", "hgemm", "hg4_", "hconv_kernel", "torgb_kernel")):
                     continue
                 c = r["Counter_Name"]
                 per[c] += float(r["Counter_Value"])
