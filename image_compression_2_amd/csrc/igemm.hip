@@ -44,6 +44,7 @@ struct IgemmArgs {
   int tiles_o;  // ceil(cout_p / BO)
   int nblocks;  // tiles_o * tiles_p
   int group;    // p-tiles per o-sweep (tile_coords)
+  int korder;   // 8-phase kernels: 0 = tap-major K, 1 = channel-major K (taps innermost)
   int act;
   float slope, act_gain, clamp, out_mul;
   int out_layout, out_dtype;
@@ -484,22 +485,39 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   struct Cur {
     int t, ky, kx, cb;
   };
+  // K order.  tap-major (cb innermost: K-tile t is the contiguous weight column t) streams a WG's whole
+  // 256-pixel x cin_p panel once per tap, so the 9 shifted re-reads of a pixel are cin_p / 64 K-tiles apart and
+  // the ~32 resident WGs of an XCD cycle ~8 MB through its 4 MB L2 between them (PMC: 5.4x the compulsory HBM
+  // bytes on s148).  channel-major (taps innermost, the halo kernels' order) re-reads each 64-channel panel at the
+  // 9 taps back to back.  IC2_IGEMM_KORDER=0 / 1 selects tap- / channel-major.
+  const bool cmaj = a.korder != 0;
   auto advance = [&](Cur c) {
     c.t += 1;
-    c.cb += 1;
-    const int wrap = c.cb == CB;
-    c.cb = wrap ? 0 : c.cb;
-    c.kx += wrap;
-    const int wrap2 = c.kx == a.kw;
-    c.kx = wrap2 ? 0 : c.kx;
-    c.ky += wrap2;
+    if (cmaj) {
+      c.kx += 1;
+      const int wrap = c.kx == a.kw;
+      c.kx = wrap ? 0 : c.kx;
+      c.ky += wrap;
+      const int wrap2 = c.ky == a.kh;
+      c.ky = wrap2 ? 0 : c.ky;
+      c.cb += wrap2;
+    } else {
+      c.cb += 1;
+      const int wrap = c.cb == CB;
+      c.cb = wrap ? 0 : c.cb;
+      c.kx += wrap;
+      const int wrap2 = c.kx == a.kw;
+      c.kx = wrap2 ? 0 : c.kx;
+      c.ky += wrap2;
+    }
     return c;
   };
 
 #define IC2_G8_ISSUE_A(h_, buf_, c_)                                                                          \
   {                                                                                                          \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(                                     \
-        (void*)(wg + (int64_t)(c_).t * 128), 0, (c_).t < a.nq ? kOob : 0, kRsrcWord3);                        \
+        (void*)(wg + (int64_t)(((c_).ky * a.kw + (c_).kx) * CB + (c_).cb) * 128), 0, (c_).t < a.nq ? kOob : 0,  \
+        kRsrcWord3);                                                                                         \
     _Pragma("unroll") for (int k = 0; k < NA; ++k)                                                           \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G::BUF + \
                                                                                        g8_arow(h_, wid_u + 8 * k, 0) * 128), \
@@ -1603,6 +1621,11 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
     return g >= 1 ? g : 1;
   }();
   a.group = group;
+  static const int korder = [] {
+    const char* e = getenv("IC2_IGEMM_KORDER");
+    return e ? atoi(e) : 1;  // channel-major: s148 +3 %, s148b +5 %, s148c +7 %, C2 +2.6 % (profiles/r2f_korder.txt)
+  }();
+  a.korder = korder;
   hipStream_t s = as_stream(stream);
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
@@ -1690,6 +1713,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = dtype;
   a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
   a.group = 1;
+  a.korder = 0;
   if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);
   else if (cin_p == 32) launch_hconv<32, 64, true>(a, s);
   else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32, true>(a, s);
