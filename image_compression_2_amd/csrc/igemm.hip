@@ -902,8 +902,10 @@ static HgPlan hg_plan(int n, int ho, int wo, int cout_p) {
 // So: cin_p, cout_p <= 256 and >= 95 % tile utilisation.  IC2_HGEMM=0 disables it, =2 forces it wherever legal.
 static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
   static const int mode = [] {
+    // default off since the channel-major K order (round 2f): the 8-phase kernel then matches or beats it on the
+    // 256-wide encoder blocks it used to win (e2b 1062 vs 1133 TF/s), and hg4 took the <= 192-wide layers
     const char* e = getenv("IC2_HGEMM");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   if (!(mode && dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 64 == 0 && cout_p % 64 == 0 &&
         x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))

@@ -381,8 +381,13 @@ def test_conv_halo_gemm(cuda, cin, cout, size, pad):
     """The halo implicit GEMM (bf16 3x3, cin_p % 64 == 0: 2-D pixel tiles whose input halo is staged once
     per 64-channel block) on every instance -- 256 / 128 output channels per workgroup, 16 x 16 / 8 x 32 pixel
     tiles, padded output-channel tails (181 -> 192, 384), ragged tile edges, pad 1 and 2 -- against
-    F.conv2d in fp64."""
-    _conv_case(cin, cout, size, pad, n=8)
+    F.conv2d in fp64.  Off in the default launch plan, so forced (IC2_HGEMM=2, hg4 off) in a child process."""
+    import subprocess, sys
+    code = (f"import sys; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
+            f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},n=8)")
+    env = dict(__import__('os').environ, IC2_HGEMM="2", IC2_HG4="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("cin,cout,size,pad", [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1),
