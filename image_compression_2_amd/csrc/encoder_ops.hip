@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) gn_apply_oct_kernel(const TI* __restrict_
       ld8(yb + (int64_t)idx * c_p, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float t = (v[k] - mu[k]) * sc[k] + sh[k];
+        float t = __builtin_fmaf(v[k] - mu[k], sc[k], sh[k]);  // as gn_lrelu_bf16x8 (igemm.hip), bit for bit
         t = t < 0.f ? t * slope : t;
         res[k] = accum ? res[k] + t : t;
       }
@@ -427,7 +427,9 @@ __global__ void __launch_bounds__(256) resize_bilinear_kernel(const float* __res
 // igemm.hip: the conv with the GroupNorm partial sums fused into the halo conv's epilogue
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                   int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
-                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s);
+                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
+                  const float* in_gn, float in_slope);
+bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad);
 int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
                                    int groups);
 
@@ -606,10 +608,10 @@ extern "C" int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w_, 
 // conv runs the layer, the per-tile (sum, sumsq) come out of its epilogue (no second read of y); otherwise the
 // separate two-stage statistics pass runs.  stats: ic2_conv3x3_gn_stats_floats() floats; the first n*groups*2 are
 // (mean, rstd) per (sample, group), as ic2_group_norm_stats writes them.
-extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
-                                  int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, int groups,
-                                  float eps, float* stats, int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes,
-                                  int fuse, void* stream) {
+static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
+                               int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, int groups,
+                               float eps, float* stats, int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes,
+                               int fuse, void* stream, const float* in_gn, float in_slope) {
   IC2_CHECK_ARG(x && w && y && stats && groups > 0 && cout_valid > 0 && cout_valid % groups == 0,
                 "conv3x3_gn_fwd: bad arguments");
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
@@ -619,7 +621,8 @@ extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dty
   const int64_t sf = ((int64_t)n * groups * 2 + 1) / 2 * 2;
   double* part = reinterpret_cast<double*>(stats + sf);
   const int nch = conv_gn_fused(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, part,
-                                (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s);
+                                (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope);
+  if (nch == -2) return IC2_E_UNSUPPORTED;
   if (nch < 0) return IC2_E_INVALID;
   if (nch == 0)
     return ic2_group_norm_stats(y, dtype, n, ho * wo, cout_p, cout_valid, groups, eps, stats, stream);
@@ -627,6 +630,59 @@ extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dty
                      (double)ho * wo * (cout_valid / groups), eps, stats);
   IC2_CHECK_LAUNCH("conv3x3_gn_fwd");
   return IC2_OK;
+}
+
+extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
+                                  int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, int groups,
+                                  float eps, float* stats, int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes,
+                                  int fuse, void* stream) {
+  return conv3x3_gn_fwd_impl(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, eps, stats,
+                             stats_floats, conv_ws, conv_ws_bytes, fuse, stream, nullptr, 0.f);
+}
+
+// (mean, rstd * gamma, beta, 0) per (sample, channel) from GroupNorm stats [n][groups][2] (mean, rstd): the operands
+// of gn_apply_oct_kernel, for a consumer that applies GroupNorm + lrelu while it loads (padded channels: 0)
+__global__ void __launch_bounds__(256) gn_affine_table_kernel(const float* __restrict__ stats,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, int n, int c, int c_p,
+                                                              int groups, float4* __restrict__ table) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * c_p) return;
+  const int ch = e % c_p, nn = e / c_p;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ch < c) {
+    const int g = ch / (c / groups);
+    v.x = stats[((int64_t)nn * groups + g) * 2 + 0];
+    v.y = stats[((int64_t)nn * groups + g) * 2 + 1] * gamma[ch];
+    v.z = beta[ch];
+  }
+  table[e] = v;
+}
+
+extern "C" int ic2_gn_affine_table(const float* stats, const float* gamma, const float* beta, int n, int c, int c_p,
+                                   int groups, float* table, void* stream) {
+  IC2_CHECK_ARG(stats && gamma && beta && table && n > 0 && c > 0 && c <= c_p && groups > 0 && c % groups == 0,
+                "gn_affine_table: bad arguments");
+  IC2_CHECK_ARG((uintptr_t)table % 16 == 0, "gn_affine_table: table must be 16-byte aligned");
+  hipLaunchKernelGGL(gn_affine_table_kernel, dim3((unsigned)ceil_div((int64_t)n * c_p, 256)), dim3(256), 0,
+                     as_stream(stream), stats, gamma, beta, n, c, c_p, groups, reinterpret_cast<float4*>(table));
+  IC2_CHECK_LAUNCH("gn_affine_table");
+  return IC2_OK;
+}
+
+extern "C" int ic2_conv3x3_gnin_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
+                                          int pad) {
+  return conv_gn_in_supported(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad) ? 1 : 0;
+}
+
+extern "C" int ic2_conv3x3_gnin_gn_fwd(const void* x, const float* in_gn, float in_slope, const void* w, void* y,
+                                       int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh,
+                                       int kw, int pad, const float* bias, int groups, float eps, float* stats,
+                                       int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse,
+                                       void* stream) {
+  IC2_CHECK_ARG(in_gn != nullptr && (uintptr_t)in_gn % 16 == 0, "conv3x3_gnin_gn_fwd: in_gn must be a 16-byte aligned table");
+  return conv3x3_gn_fwd_impl(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, eps, stats,
+                             stats_floats, conv_ws, conv_ws_bytes, fuse, stream, in_gn, in_slope);
 }
 
 extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p,

@@ -52,6 +52,10 @@ struct IgemmArgs {
   // the stored (rounded) outputs of channels < gn_c; null = off
   double* gn_part;
   int gn_groups, gn_c;
+  // GroupNorm + lrelu of the INPUT applied while the halo conv stages it (hconv, cin_p 32 / 64 only): per
+  // (sample, input channel) (mean, rstd * gamma, beta, 0) f32 [n][cin_p][4]; null = the input is used as is
+  const float* in_gn;
+  float in_slope;
 };
 
 template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
@@ -1287,6 +1291,23 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
 // Wave w of 8 owns pixel blocks {w, w+8, ...} (16 pixels of one row) x every 16-channel o-block:
 // A = weights (lane: o = 16i + fr, k = 8 fh .. +7), B = halo pixels (lane: pixel fr, k = 8 fh .. +7).
 // Epilogue = ig_store4 (same oscale / bias / activation / output layouts as the implicit GEMM).
+// lrelu((v - mean) * scale + shift) on 8 bf16 values, rounded back to bf16: the arithmetic of
+// gn_apply_oct_kernel (encoder_ops.hip) on the same operands, so a fused input equals the materialised one bit for bit
+__device__ __forceinline__ uint4 gn_lrelu_bf16x8(uint4 u, const float4 (&p)[8], float slope) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float lo = __uint_as_float(w[k] << 16), hi = __uint_as_float(w[k] & 0xffff0000u);
+    lo = __builtin_fmaf(lo - p[2 * k].x, p[2 * k].y, p[2 * k].z);
+    hi = __builtin_fmaf(hi - p[2 * k + 1].x, p[2 * k + 1].y, p[2 * k + 1].z);
+    lo = lo < 0.f ? lo * slope : lo;
+    hi = hi < 0.f ? hi * slope : hi;
+    o[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int CINP, int COUTP, int TH>
 struct HcCfg {
   static constexpr int TW = 32, HR = TH + 2, HC = TW + 2;
@@ -1321,12 +1342,19 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
 
   const char* xg = reinterpret_cast<const char*>(a.x);
   uint4 pre[C::PER_T];
+  // input GroupNorm + lrelu (a.in_gn; the 64-channel instances only -- the 32-channel ones run at 4 waves per SIMD
+  // and would spill the 32 extra VGPRs): 512 % 8 == 0, so a thread's pieces all hold channels (tid % 8) * 8 .. +7,
+  // whose (mean, scale, shift) are loaded once per tile
+  constexpr bool kGnIn = CINP == 64;
+  float4 gnp[8];
+  uint32_t inimg = 0;
   auto fetch = [&](int t) {
     const int tx = t % tiles_x;
     const int t2 = t / tiles_x;
     const int ty = t2 % tiles_y;
     const int nn = t2 / tiles_y;
     const int y0 = ty * TH - a.pad, x0 = tx * C::TW - a.pad;
+    inimg = 0;
 #pragma unroll
     for (int k = 0; k < C::PER_T; ++k) {
       const int e = tid + 512 * k;
@@ -1334,8 +1362,16 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
       const int hr = pi / C::HC, hc = pi - hr * C::HC;
       const int iy = y0 + hr, ix = x0 + hc;
       const bool ok = e < C::NPIECE && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
+      inimg |= (uint32_t)ok << k;
       pre[k] = ok ? *reinterpret_cast<const uint4*>(xg + ((((int64_t)nn * a.h + iy) * a.w_ + ix) * CINP + part * 8) * 2)
                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if constexpr (kGnIn) {
+      if (a.in_gn) {
+        const float4* tb = reinterpret_cast<const float4*>(a.in_gn) + ((int64_t)nn * CINP + (tid % (CINP / 8)) * 8);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) gnp[c] = tb[c];
+      }
     }
   };
   if (blockIdx.x < ntiles) fetch(blockIdx.x);
@@ -1347,7 +1383,11 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
       const int e = tid + 512 * k;
       if (e < C::NPIECE) {
         const int pi = e / (CINP / 8), part = e - pi * (CINP / 8);
-        *reinterpret_cast<uint4*>(halo + pi * C::PPB + part * 16) = pre[k];
+        uint4 v = pre[k];
+        if constexpr (kGnIn) {  // zero padding stays zero: only in-image pieces are normalised
+          if (a.in_gn && ((inimg >> k) & 1u)) v = gn_lrelu_bf16x8(v, gnp, a.in_slope);
+        }
+        *reinterpret_cast<uint4*>(halo + pi * C::PPB + part * 16) = v;
       }
     }
     __syncthreads();
@@ -1617,6 +1657,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
   a.out_layout = out_layout; a.out_dtype = out_dtype;
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
+  a.in_gn = nullptr; a.in_slope = 0.f;
   static const int group = [] {
     const char* e = getenv("IC2_IGEMM_GROUP");
     const int g = e ? atoi(e) : 1;  // 1 = o-tiles of a p-tile side by side (measured best)
@@ -1683,9 +1724,16 @@ namespace ic2 {
 // kernel is the one the dispatcher picks.  Returns the number of per-image chunks written to `part`
 // ([n][groups][chunks][2] f64), 0 when the conv ran unfused (the caller then computes the statistics itself),
 // or -1 on an argument error (message set).
+bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (dtype != IC2_BF16 || cin_p != 64 || ho <= 0 || wo <= 0) return false;
+  return hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw);
+}
+
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                   int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
-                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s) {
+                  int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
+                  const float* in_gn, float in_slope) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
   const bool hconv = hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
@@ -1699,9 +1747,14 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     const char* e = getenv("IC2_CONV_GN");
     return e && e[0] == '1';
   }();
-  const bool fuse = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
-  if (!fuse || !hconv || part == nullptr || part_doubles < (int64_t)n * groups * nch * 2 || groups != 32 ||
-      cout_valid != cout_p || bias == nullptr) {
+  const bool fuse_req = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
+  const bool fuse = fuse_req && hconv && part != nullptr && part_doubles >= (int64_t)n * groups * nch * 2 &&
+                    groups == 32 && cout_valid == cout_p && bias != nullptr;
+  if (in_gn != nullptr && !conv_gn_in_supported(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad)) {
+    set_error("conv3x3_gn_fwd: input GroupNorm fusion needs the halo conv (bf16, cin_p 64)");
+    return -2;
+  }
+  if (!fuse && in_gn == nullptr) {
     const int rc = ic2_conv_igemm_ws(x, w, y, dtype, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo,
                                      nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace, ws_bytes, s);
     return rc == IC2_OK ? 0 : -1;
@@ -1713,16 +1766,24 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
   a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = 1.f;
   a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = dtype;
-  a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
+  a.gn_part = fuse ? part : nullptr; a.gn_groups = groups; a.gn_c = cout_valid;
   a.group = 1;
   a.korder = 0;
-  if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);
-  else if (cin_p == 32) launch_hconv<32, 64, true>(a, s);
-  else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32, true>(a, s);
-  else if (cin_p == 64) launch_hconv<64, 64, true>(a, s);
-  else if (cout_p == 32) launch_hconv<96, 32, true>(a, s);
-  else launch_hconv<96, 64, true>(a, s);
-  return (int)nch;
+  a.in_gn = in_gn; a.in_slope = in_slope;
+  if (fuse) {
+    if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);
+    else if (cin_p == 32) launch_hconv<32, 64, true>(a, s);
+    else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32, true>(a, s);
+    else if (cin_p == 64) launch_hconv<64, 64, true>(a, s);
+    else if (cout_p == 32) launch_hconv<96, 32, true>(a, s);
+    else launch_hconv<96, 64, true>(a, s);
+    return (int)nch;
+  }
+  if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
+  else if (cin_p == 32) launch_hconv<32, 64>(a, s);
+  else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
+  else launch_hconv<64, 64>(a, s);
+  return 0;
 }
 
 int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,

@@ -80,6 +80,10 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
 
 # IC2_FROM_RGB_DIRECT=0 keeps the packing + implicit-GEMM from_rgb (A/B switch)
 _FROM_RGB_DIRECT = os.environ.get("IC2_FROM_RGB_DIRECT", "1") != "0"
+# IC2_GN_IN_FUSE=1 applies norm1 + lrelu inside conv2's halo-conv staging instead of materialising it.  Bit-identical
+# but measured level on MI355X (C2 1438.0 -> 1439.4, C4 415.5 -> 415.9 img/s, same box: the saved pass is paid back in
+# the heavier staging of the 64-channel halo conv), so off by default
+_GN_IN_FUSE = os.environ.get("IC2_GN_IN_FUSE", "0") == "1"
 
 
 def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream):
@@ -98,9 +102,10 @@ def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream):
     return _conv(conv, _to_nhwc(x, dt, stream), dt, cache, stream)
 
 
-def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stream, fuse=-1):
+def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stream, fuse=-1, in_gn=None):
     """conv (+ bias) and the GroupNorm statistics of its output in one call (ic2_conv3x3_gn_fwd: fused into the
-    halo conv's epilogue where that kernel runs the layer).  -> (y, stats)."""
+    halo conv's epilogue where that kernel runs the layer).  in_gn = (affine table, slope): the previous GroupNorm +
+    lrelu applied to x while the halo conv stages it (ic2_conv3x3_gnin_gn_fwd).  -> (y, stats)."""
     cout, cin, kh, kw = conv.weight.shape
     pad = conv.padding[0]
     wp, bp = _packed(conv, x, dt, cache, stream)
@@ -112,9 +117,30 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
     nbytes = int(nv.query("ic2_conv_igemm_ws_bytes", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad))
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=x.t.device) if nbytes > 0 else None
-    nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), dc, x.n, x.h, x.w, x.c_p, cout_p, cout, kh, kw,
-            pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, nv.ptr(ws), nbytes, int(fuse), stream)
+    if in_gn is not None:
+        nv.call("ic2_conv3x3_gnin_gn_fwd", nv.ptr(x.t), nv.ptr(in_gn[0]), float(in_gn[1]), nv.ptr(wp), nv.ptr(y), dc,
+                x.n, x.h, x.w, x.c_p, cout_p, cout, kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps),
+                nv.ptr(stats), nfl, nv.ptr(ws), nbytes, int(fuse), stream)
+    else:
+        nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), dc, x.n, x.h, x.w, x.c_p, cout_p, cout, kh,
+                kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, nv.ptr(ws), nbytes,
+                int(fuse), stream)
     return _Act(y, cout), stats
+
+
+def _gn_in_fusable(conv: nn.Conv2d, y: _Act, dt):
+    """Can conv consume lrelu(GroupNorm(y)) through ic2_conv3x3_gnin_gn_fwd (the halo conv runs the shape)?"""
+    cout, cin, kh, kw = conv.weight.shape
+    return (_GN_IN_FUSE and dt == torch.bfloat16 and y.t.dtype == torch.bfloat16 and
+            bool(nv.query("ic2_conv3x3_gnin_supported", nv.BF16, y.n, y.h, y.w, y.c_p, nv.pad32(cout), kh, kw,
+                          conv.padding[0])))
+
+
+def _gn_affine_table(norm: nn.GroupNorm, y: _Act, stats, stream):
+    table = torch.empty([y.n, y.c_p, 4], dtype=torch.float32, device=y.t.device)
+    nv.call("ic2_gn_affine_table", nv.ptr(stats), nv.ptr(norm.weight), nv.ptr(norm.bias), y.n, y.c, y.c_p,
+            norm.num_groups, nv.ptr(table), stream)
+    return table
 
 
 def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None):
@@ -287,8 +313,13 @@ class VGGBlock(nn.Module):
 
     def run_nhwc(self, x: _Act, dt, cache, stream):
         y, st = _conv_gn(self.conv1, self.norm1, x, dt, cache, stream)
-        h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st)
-        y, st = _conv_gn(self.conv2, self.norm2, h, dt, cache, stream)
+        if _gn_in_fusable(self.conv2, y, dt):
+            # norm1 + lrelu applied while conv2's halo conv stages its input: lrelu(norm1(y)) never reaches HBM
+            y, st = _conv_gn(self.conv2, self.norm2, y, dt, cache, stream,
+                             in_gn=(_gn_affine_table(self.norm1, y, st, stream), 0.2))
+        else:
+            h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st)
+            y, st = _conv_gn(self.conv2, self.norm2, h, dt, cache, stream)
         pool = y.h > 1 and y.w > 1
         return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st)
 

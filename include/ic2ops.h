@@ -279,6 +279,20 @@ int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, 
                        int cout_valid, int kh, int kw, int pad, const float* bias, int groups, float eps, float* stats,
                        int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse, void* stream);
 
+/* VGGBlock's second conv with the first GroupNorm + lrelu applied to its INPUT as the halo conv stages it
+ * (stylegan3_hvae_full.py:183-191: conv2(lrelu(norm1(conv1(x))))): the normalised activation is never written to
+ * HBM.  x = conv1's raw output (bf16 NHWC, cin_p 64); in_gn = ic2_gn_affine_table() of norm1 [n][cin_p][4] f32;
+ * in_slope = the lrelu slope; zero padding stays zero (the reference pads the normalised activation).  Otherwise as
+ * ic2_conv3x3_gn_fwd.  Bit-identical to ic2_gn_lrelu_pool (no pool) followed by ic2_conv3x3_gn_fwd.  Returns
+ * IC2_E_UNSUPPORTED unless ic2_conv3x3_gnin_supported() (the halo conv runs the shape). */
+int ic2_conv3x3_gnin_supported(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad);
+int ic2_gn_affine_table(const float* stats, const float* gamma, const float* beta, int n, int c, int c_p, int groups,
+                        float* table, void* stream);
+int ic2_conv3x3_gnin_gn_fwd(const void* x, const float* in_gn, float in_slope, const void* w, void* y, int dtype, int n,
+                            int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                            const float* bias, int groups, float eps, float* stats, int64_t stats_floats, void* conv_ws,
+                            int64_t conv_ws_bytes, int fuse, void* stream);
+
 /* Backward of ic2_flrelu_nhwc w.r.t. its input (SynthesisLayer's filtered_lrelu, SG3-public; the encoder's loss
  * reaches W+ through it, :669-696): x = the forward's input (NHWC [n][in_h][in_w][c_p], f32 or f16), gout = the
  * gradient of its output (NHWC [n][out_h][out_w][c_p], f32 or bf16) -> gx (NHWC, f32).  Recomputes the upsampled

@@ -406,6 +406,38 @@ def test_conv_halo_gemm4(cuda, cin, cout, size, pad):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("cin,h,w", [(32, 130, 131), (64, 129, 130)])
+def test_vggblock_gn_input_fusion_bit_identical(cuda, cin, h, w):
+    """VGGBlock.run_nhwc in bf16 with norm1 + lrelu fused into conv2's halo-conv input staging
+    (ic2_conv3x3_gnin_gn_fwd) gives the same bits as the materialised lrelu(norm1(conv1)) path (ragged tiles and
+    the zero padding of the normalised activation included), and the fused path is the one that ran."""
+    from image_compression_2_amd import stylegan3_hvae_full as shf
+    g = torch.Generator().manual_seed(cin + h)
+    torch.manual_seed(cin + h)
+    blk = shf.VGGBlock(cin, 64).to(cuda)
+    with torch.no_grad():
+        for nrm in (blk.norm1, blk.norm2):
+            nrm.weight.copy_(torch.rand(64, generator=g) + 0.5)
+            nrm.bias.copy_(torch.randn(64, generator=g) * 0.3)
+    n = 4
+    x = (torch.randn(n, h, w, cin, generator=g) * 2).to(torch.bfloat16).to(cuda)
+    xa = shf._Act(x, cin)
+    stream = nv.stream_of(x)
+    y1, _ = shf._conv_gn(blk.conv1, blk.norm1, xa, torch.bfloat16, {}, stream)
+    saved = shf._GN_IN_FUSE
+    outs = []
+    try:
+        for fuse in (True, False):
+            shf._GN_IN_FUSE = fuse
+            assert shf._gn_in_fusable(blk.conv2, y1, torch.bfloat16) == fuse
+            with torch.no_grad():
+                outs.append(blk.run_nhwc(xa, torch.bfloat16, {}, stream).t.clone())
+    finally:
+        shf._GN_IN_FUSE = saved
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("cin,cout,n,h,w", [(3, 32, 3, 67, 45), (3, 64, 2, 40, 33), (1, 32, 1, 9, 70), (4, 32, 2, 16, 32)])
 def test_from_rgb_direct(cuda, cin, cout, n, h, w):
     """ic2_from_rgb_conv (from_rgb read straight from the NCHW f32 image, bf16 NHWC out) against F.conv2d in fp64
