@@ -230,15 +230,24 @@ __global__ void __launch_bounds__(NT) flrelu_bwd_kernel(FlrBwdArgs a) {
       bf2v os = bf2v{1.f, 1.f}, bi = bf2v{0.f, 0.f};
       if (a.oscale) os = bf2v{a.oscale[(int64_t)n * a.c_p + c], a.oscale[(int64_t)n * a.c_p + c + 1]};
       if (a.bias) bi = bf2v{a.bias[c], a.bias[c + 1]};
+      // the ydot operand x of every row BEFORE the first gx store: a load placed after a store to gx may alias
+      // it, which serialised one round trip per row (vmcnt(0) per row in the up-4 instances)
+      if (a.ydot) {
+        bf2v xv[RG];
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+          const int gyy = i0y + rg * RG + r;
+          xv[r] = ldp<TI>(xin + ((int64_t)gyy * a.in_w + gxx) * a.c_p + c, gyy < a.in_h);
+        }
+#pragma unroll
+        for (int r = 0; r < RG; ++r)
+          if (i0y + rg * RG + r < a.in_h) ydp += o[r] * (xv[r] - bi);
+      }
 #pragma unroll
       for (int r = 0; r < RG; ++r) {
         const int gyy = i0y + rg * RG + r;
         if (gyy >= a.in_h) continue;
         const int64_t e = ((int64_t)gyy * a.in_w + gxx) * a.c_p + c;
-        if (a.ydot) {
-          const bf2v xv = ldp<TI>(xin + e, true);
-          ydp += o[r] * (xv - bi);
-        }
         const bf2v v = o[r] * os;
         if (a.out_bf16) {
           bf16_t* po = reinterpret_cast<bf16_t*>(a.gx) + (int64_t)n * a.in_h * a.in_w * a.c_p + e;
