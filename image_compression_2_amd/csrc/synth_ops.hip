@@ -293,27 +293,38 @@ template <bool OSCALE>
 __device__ __forceinline__ void small_mm_body(const float* __restrict__ a, int64_t lda, const float* __restrict__ w,
                                               int n, int K, int nout, int out_p, float* __restrict__ out,
                                               const ModLayer& L) {
-  __shared__ float wl[16][kSmK + 1];
-  __shared__ float al[16][kSmK + 1];
+  // rows zero-padded to K4 (a multiple of 4) at a pitch of kSmK + 4 floats: 16-B aligned ds_read_b128 of 16
+  // different rows land in 16 distinct 16-B bank slots (pitch = 16 mod 256 B)
+  constexpr int P = kSmK + 4;
+  __shared__ __attribute__((aligned(16))) float wl[16][P];
+  __shared__ __attribute__((aligned(16))) float al[16][P];
   const int t = threadIdx.x;
   const int o0 = blockIdx.x * 16;
-  for (int e = t; e < 16 * K; e += 256) {
-    const int r = e / K, i = e - (e / K) * K;
-    wl[r][i] = o0 + r < nout ? w[(int64_t)(o0 + r) * K + i] : 0.f;
+  const int K4 = (K + 3) & ~3;
+  for (int e = t; e < 16 * K4; e += 256) {
+    const int r = e / K4, i = e - (e / K4) * K4;
+    wl[r][i] = o0 + r < nout && i < K ? w[(int64_t)(o0 + r) * K + i] : 0.f;
   }
   const int ol = t & 15, nl = t >> 4;
   const int o = o0 + ol;
   for (int n0 = 0; n0 < n; n0 += 16) {
     __syncthreads();  // weights staged / previous chunk consumed
-    for (int e = t; e < 16 * K; e += 256) {
-      const int r = e / K, i = e - (e / K) * K;
-      float v = n0 + r < n ? a[(int64_t)(n0 + r) * lda + i] : 0.f;
+    for (int e = t; e < 16 * K4; e += 256) {
+      const int r = e / K4, i = e - (e / K4) * K4;
+      float v = n0 + r < n && i < K ? a[(int64_t)(n0 + r) * lda + i] : 0.f;
       if (OSCALE) v = v * v;
       al[r][i] = v;
     }
     __syncthreads();
-    float acc = 0.f;
-    for (int i = 0; i < K; ++i) acc = fmaf(al[nl][i], wl[ol][i], acc);
+    float acc = 0.f;  // sequential over i (fixed order)
+    for (int i = 0; i < K4; i += 4) {
+      const float4 av = *reinterpret_cast<const float4*>(&al[nl][i]);
+      const float4 wv = *reinterpret_cast<const float4*>(&wl[ol][i]);
+      acc = fmaf(av.x, wv.x, acc);
+      acc = fmaf(av.y, wv.y, acc);
+      acc = fmaf(av.z, wv.z, acc);
+      acc = fmaf(av.w, wv.w, acc);
+    }
     const int nn = n0 + nl;
     if (nn < n && o < out_p) {
       float v;
