@@ -937,7 +937,7 @@ static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int
 //   LDS rows of 64 B, 16-B chunk c stored at c ^ (((row >> 2) & 1) << 1): conflict-free ds_read_b128 for 16
 //   consecutive rows starting at ANY row (the halo fragments start at tap-shifted rows), checked by brute force
 //   over the four ds_read_b128 lane groups.
-template <int I, int J, int WGO, int WGP, int TW, int NS>
+template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false>
 struct H4 {
   static constexpr int BO = 16 * I * WGO, BP = 16 * J * WGP, TH = BP / TW;
   static constexpr int HW = TW + 2, HH = TH + 2, NH = HH * HW;  // halo pixels
@@ -946,7 +946,7 @@ struct H4 {
   static constexpr int HALO_B = NHI * 1024;
   static constexpr int WS_B = BO * 64;                          // one weight slab: BO rows x 32 channels
   static constexpr int NWI = (BO / 16 + 3) / 4;                 // weight DMA instructions per wave
-  static constexpr int LDS_B = NS * WS_B + 2 * HALO_B;  // NS-slab weight ring
+  static constexpr int LDS_B = NS * WS_B + 2 * HALO_B + (HB ? 1024 : 0);  // NS-slab weight ring (+ HB dummy slot)
   static_assert(BP % TW == 0 && TW % 16 == 0, "pixel tile");
   static_assert((BO / 16) % 4 == 0, "weight slab rows split evenly over the 4 waves");
   static_assert(HPW <= 8, "halo DMA spread over the first 8 taps");
@@ -954,9 +954,12 @@ struct H4 {
 };
 __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
 
-template <int I, int J, int WGO, int WGP, int TW, int NS>
+// HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
+// past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
+// chain, ~60 SALU per step) and a wait count that depends only on the tap
+template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
-  using G = H4<I, J, WGO, WGP, TW, NS>;
+  using G = H4<I, J, WGO, WGP, TW, NS, HB>;
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
   constexpr int NWI = G::NWI, HPW = G::HPW;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
@@ -1021,6 +1024,15 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 4 * k) * 1024),
                                                16, w_off[k], 0, 0, 0);
   };
+  auto issue_hb = [&](int cb) {  // HB: all HPW DMAs of this wave for the halo of block cb -> halo cb & 1 (or dummy)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 64), 0, kOob, kRsrcWord3);
+#pragma unroll
+    for (int k = 0; k < HPW; ++k) {
+      char* dst = wid + 4 * k < G::NHI ? hal + (cb & 1) * G::HALO_B + (wid + 4 * k) * 1024 : hal + 2 * G::HALO_B;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, h_off[k], 0, 0, 0);
+    }
+  };
   auto issue_h1 = [&](int cb, int k) {  // DMA k of this wave for the halo of block cb -> halo cb & 1
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 64), 0, kOob, kRsrcWord3);
@@ -1047,10 +1059,12 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     const int cb = t / 9, tap = t - (t / 9) * 9;
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
     issue_w(t + LA);  // slab (t+LA) % NS was last read by step t-1
-    // one DMA of the next block's halo per step over the block's first taps (halo (cb+1) & 1 was last read
-    // by block cb-1); wave-uniform condition
-    const bool hdma = tap < HPW && cb + 1 < CB && wid + 4 * tap < G::NHI;
-    if (hdma) {
+    // the next block's halo (halo (cb+1) & 1 was last read by block cb-1): HB one burst at tap 0, else one DMA
+    // per step over the block's first taps; wave-uniform conditions
+    const bool hdma = !HB && tap < HPW && cb + 1 < CB && wid + 4 * tap < G::NHI;
+    if constexpr (HB) {
+      if (tap == 0 && cb + 1 < CB) issue_hb(cb + 1);
+    } else if (hdma) {
 #pragma unroll
       for (int k = 0; k < HPW; ++k)
         if (k == tap) issue_h1(cb + 1, k);
@@ -1076,8 +1090,13 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     // slab t+1 (issued at step t+1-LA) landed; the DMAs of the last LA-1 steps may stay in flight (each step
     // issues NWI weight DMAs and, on the block's first taps, one halo DMA; counting the halo DMAs of earlier
     // steps as landed is conservative: vmcnt retires in issue order)
-    if (hdma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");
+    if constexpr (HB) {  // a burst issued within the last LA-1 steps (tap < LA-1 of a block that issued one)
+      if (tap < LA - 1 && cb + 1 < CB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI + HPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");
+    } else {
+      if (hdma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail (zero-size) DMAs before the epilogue
 
@@ -1111,6 +1130,11 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
                                                                                           int ty) {            \
     hg4_body<I, J, WGO, WGP, TW, NS>(a, tx, ty);                                                                 \
   }
+#define IC2_HG4_KERNEL_HB(name, I, J, WGO, WGP, TW, NS)                                                          \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
+                                                                                          int ty) {            \
+    hg4_body<I, J, WGO, WGP, TW, NS, true>(a, tx, ty);                                                           \
+  }
 IC2_HG4_KERNEL(hg4_o128_w32_kernel, 8, 4, 1, 4, 32, 3)    // 128 o x (8 x 32) px
 IC2_HG4_KERNEL(hg4_o128_w16_kernel, 8, 4, 1, 4, 16, 3)    // 128 o x (16 x 16) px
 IC2_HG4_KERNEL(hg4_o192_w32_kernel, 6, 4, 2, 2, 32, 3)    // 192 o x (4 x 32) px
@@ -1123,7 +1147,11 @@ IC2_HG4_KERNEL(hg4_o192_w32_s4_kernel, 6, 4, 2, 2, 32, 4)
 IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)
 IC2_HG4_KERNEL(hg4_o64_w32_s4_kernel, 4, 4, 1, 4, 32, 4)   // 64 o x (8 x 32) px: the 64-wide layers
 IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)
+IC2_HG4_KERNEL_HB(hg4_o128_w32_hb_kernel, 8, 4, 1, 4, 32, 4)
+IC2_HG4_KERNEL_HB(hg4_o192_w32_hb_kernel, 6, 4, 2, 2, 32, 4)
+IC2_HG4_KERNEL_HB(hg4_o64_w32_hb_kernel, 4, 4, 1, 4, 32, 4)
 #undef IC2_HG4_KERNEL
+#undef IC2_HG4_KERNEL_HB
 
 static int hg4_env(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -1162,7 +1190,14 @@ static void launch_hg4(IgemmArgs a, hipStream_t s, void (*kern)(IgemmArgs, int, 
 
 static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
   static const int ns = hg4_env("IC2_HG4_NS", 4);  // 4-slab ring: +0.5-1 % over 3 (profiles/r2e_hg4_sweep.txt)
+  static const int hb = hg4_env("IC2_HG4_HB", 1);  // halo burst: s276a +2.6 %, s276b +3 %, T11 +7 % (profiles/r2f_hg4_hb.txt)
   const H4Plan p = h4_plan(a.n, a.ho, a.wo, a.cout_p);
+  if (hb && ns == 4 && p.tw32 && p.bo != 256) {
+    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, hg4_o192_w32_hb_kernel);
+    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_hb_kernel);
+    else launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_hb_kernel);
+    return;
+  }
   if (p.bo == 256) {
     if (p.tw32) launch_hg4<8, 4, 2, 2, 32>(a, s, hg4_o256_w32_kernel);
     else launch_hg4<8, 4, 2, 2, 16>(a, s, hg4_o256_w16_kernel);
