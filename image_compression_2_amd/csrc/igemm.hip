@@ -514,6 +514,12 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
       c.kx = wrap2 ? 0 : c.kx;
       c.ky += wrap2;
     }
+    // the selects above come out as v_cndmask: without this the compiler treats the cursor as divergent and wraps
+    // every DMA whose descriptor derives from it in a readfirstlane waterfall loop
+    c.t = __builtin_amdgcn_readfirstlane(c.t);
+    c.ky = __builtin_amdgcn_readfirstlane(c.ky);
+    c.kx = __builtin_amdgcn_readfirstlane(c.kx);
+    c.cb = __builtin_amdgcn_readfirstlane(c.cb);
     return c;
   };
 
