@@ -45,6 +45,7 @@ struct IgemmArgs {
   int nblocks;  // tiles_o * tiles_p
   int group;    // p-tiles per o-sweep (tile_coords)
   int korder;   // 8-phase kernels: 0 = tap-major K, 1 = channel-major K (taps innermost)
+  int o_base;   // 8-phase kernels: first output channel of this launch (a cout_p split over two tile shapes)
   int act;
   float slope, act_gain, clamp, out_mul;
   int out_layout, out_dtype;
@@ -441,7 +442,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   const int logical = xcd_remap(blockIdx.x, a.nblocks);
   int o_tile, p_tile;
   tile_coords(logical, a.tiles_o, a.nblocks / a.tiles_o, a.group, o_tile, p_tile);
-  const int o0 = o_tile * G::BO;
+  const int o0 = a.o_base + o_tile * G::BO;  // o_base: a launch covering output channels [o_base, ...) only
   const int m0 = p_tile * G::BP;
   const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
   const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
@@ -666,8 +667,9 @@ static void launch_igemm(IgemmArgs a, int splits, hipStream_t s) {
 }
 
 template <int OG>
-static void launch_g8(IgemmArgs a, hipStream_t s) {
-  a.tiles_o = (a.cout_p + G8<OG>::BO - 1) / G8<OG>::BO;
+static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1) {
+  a.o_base = o_base;
+  a.tiles_o = ((o_end < 0 ? a.cout_p : o_end) - o_base + G8<OG>::BO - 1) / G8<OG>::BO;
   a.nq = a.K / 64;
   a.nblocks = (int)(ceil_div(a.M, G8<OG>::BP) * a.tiles_o);
   if constexpr (OG == 2) hipLaunchKernelGGL(igemm8_og2_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
@@ -1710,6 +1712,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
     return e ? atoi(e) : 1;  // channel-major: s148 +3 %, s148b +5 %, s148c +7 %, C2 +2.6 % (profiles/r2f_korder.txt)
   }();
   a.korder = korder;
+  a.o_base = 0;
   hipStream_t s = as_stream(stream);
   IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
@@ -1741,7 +1744,19 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   } else if (dtype == IC2_BF16) {
     switch (pl.tile) {
       case 6: launch_g8<2>(a, s); break;
-      case 7: launch_g8<1>(a, s); break;
+      case 7: {
+        // an odd multiple of 128 above 128 (384: SG3-T-256 L9, SG3-T-1024 L7): the 256-wide tile on all but the
+        // last 128 channels, the 128 x 512 tile on those (both read the same input panel); IC2_IGEMM_SPLIT=0 keeps
+        // one 128 x 512 launch
+        static const bool split = !ig_env_off("IC2_IGEMM_SPLIT");
+        if (split && cout_p % 256 == 128 && cout_p > 128 && ceil_div(M, 256) >= 240) {
+          launch_g8<2>(a, s, 0, cout_p - 128);
+          launch_g8<1>(a, s, cout_p - 128, cout_p);
+        } else {
+          launch_g8<1>(a, s);
+        }
+        break;
+      }
       case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, pl.splits, s); break;
       case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, pl.splits, s); break;
       case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, pl.splits, s); break;
@@ -1810,6 +1825,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   a.gn_part = fuse ? part : nullptr; a.gn_groups = groups; a.gn_c = cout_valid;
   a.group = 1;
   a.korder = 0;
+  a.o_base = 0;
   a.in_gn = in_gn; a.in_slope = in_slope;
   if (fuse) {
     if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);

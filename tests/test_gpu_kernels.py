@@ -406,6 +406,13 @@ def test_conv_halo_gemm4(cuda, cin, cout, size, pad):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("cin,cout,size,pad", [(128, 362, 88, 2), (96, 384, 81, 1)])
+def test_conv_split_384(cuda, cin, cout, size, pad):
+    """cout_p 384 at a large M runs as two 8-phase launches (256-wide tile on channels 0-255, 128 x 512 tile on
+    256-383, o_base): against F.conv2d in fp64, padded channels 362 -> 384 included."""
+    _conv_case(cin, cout, size, pad, n=8)
+
+
 @pytest.mark.parametrize("cin,h,w", [(32, 130, 131), (64, 129, 130)])
 def test_vggblock_gn_input_fusion_bit_identical(cuda, cin, h, w):
     """VGGBlock.run_nhwc in bf16 with norm1 + lrelu fused into conv2's halo-conv input staging
