@@ -19,30 +19,55 @@ def is_conv(name):
     return ("igemm" in name or "hgemm" in name or "hg4" in name or "hconv" in name or "torgb" in name) and "splitk" not in name
 
 
+def dispatches_per_call(ci, co, s, pad, n=32):
+    """Conv-body dispatches of one ic2_conv_igemm call: 2 where the launch plan splits an odd multiple of 128
+    output channels (> 128) over the 256-wide and the 128 x 512 8-phase tiles (igemm.hip, IC2_IGEMM_SPLIT)."""
+    cop = (co + 31) // 32 * 32 if co <= 128 else (co + 63) // 64 * 64
+    ho = s + 2 * pad - 2
+    m = n * ho * ho
+    return 2 if (cop % 256 == 128 and cop > 128 and -(-m // 256) >= 240 and ci > 256) else 1
+
+
 def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     kname = {}
+    # dispatch index -> (shape, call): walk the shapes' calls, each of dispatches_per_call dispatches
+    order = []
+    for name, ci, co, s, pad in SHAPES:
+        for _ in range(reps):
+            order.append((name, dispatches_per_call(ci, co, s, pad)))
+
+    def calls(ids):
+        i = 0
+        for name, dpc in order:
+            if i + dpc > len(ids):
+                return
+            yield name, ids[i:i + dpc]
+            i += dpc
+
     for d in sorted(glob.glob(sys.argv[1])):
         rows = {}
         for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 if is_conv(r["Kernel_Name"]):
                     rows.setdefault(int(r["Dispatch_Id"]), []).append(r)
-        for i, did in enumerate(sorted(rows)):
-            shape = SHAPES[i // reps][0] if i // reps < len(SHAPES) else "?"
-            kname[shape] = rows[did][0]["Kernel_Name"].split("(")[0]
-            for r in rows[did]:
-                per[shape][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for shape, dids in calls(sorted(rows)):
+            kname[shape] = "+".join(rows[did][0]["Kernel_Name"].split("(")[0] for did in dids)
+            tot = collections.defaultdict(float)
+            for did in dids:
+                for r in rows[did]:
+                    tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            for k, v in tot.items():
+                per[shape][k].append(v)
         trace = {}
         for f in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 if is_conv(r["Kernel_Name"]):
                     trace[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        for i, did in enumerate(sorted(trace)):
-            if i // reps < len(SHAPES):
-                dur[SHAPES[i // reps][0]].append(trace[did])
+        for shape, dids in calls(sorted(trace)):
+            dur[shape].append(sum(trace[did] for did in dids))
     out = {}
     for name, ci, co, s, pad in SHAPES:
         c = {k: sum(v) / len(v) for k, v in per[name].items()}

@@ -24,13 +24,17 @@ def main():
     kinds = collections.Counter()
     for d in sorted(glob.glob(pat)):
         for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
-            for r in csv.DictReader(open(f)):
+            rows = [r for r in csv.DictReader(open(f))
+                    if any(t in r["Kernel_Name"] for t in ("igemm", "hgemm", "hg4_", "hconv_kernel", "torgb_kernel"))]
+            names = {int(r["Dispatch_Id"]): r["Kernel_Name"] for r in rows}
+            for r in rows:
                 k = r["Kernel_Name"]
-                if not any(t in k for t in ("igemm", "hgemm", "hg4_", "hconv_kernel", "torgb_kernel")):
-                    continue
                 c = r["Counter_Name"]
                 per[c] += float(r["Counter_Value"])
-                if "splitk_reduce" not in k:
+                # one ic2_conv_igemm call = one conv-body dispatch, except the split 384-wide layers (an 8-phase
+                # 256-wide dispatch directly followed by a 128 x 512 one) and the split-K combine kernel
+                split_tail = "igemm8_og1" in k and "igemm8_og2" in names.get(int(r["Dispatch_Id"]) - 1, "")
+                if "splitk_reduce" not in k and not split_tail:
                     calls[c] += 1
                     kinds[k.split("(")[0]] += 1
     if "FETCH_SIZE" not in per or "WRITE_SIZE" not in per:
