@@ -43,6 +43,42 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert rc == 1
 
 
+def test_round2_entry_points_validate_before_launch():
+    """The batched modulation prep, the direct from_rgb, the GroupNorm affine table and the GroupNorm-input conv
+    reject bad arguments (IC2_E_INVALID / IC2_E_UNSUPPORTED + message) before any HIP call."""
+    import ctypes
+    import numpy as np
+    lib = nv.load()
+    rec = np.zeros([21, 16], dtype=np.int64)
+    # 21 layers > 20
+    assert lib.ic2_modconv_prep_batched(ctypes.c_void_p(16), 512 * 16, 2, 512, 21, rec.ctypes.data_as(ctypes.c_void_p),
+                                        None) == 1
+    assert b"nl=21" in lib.ic2_last_error()
+    # a record with null pointers
+    assert lib.ic2_modconv_prep_batched(ctypes.c_void_p(16), 512 * 16, 2, 512, 1, rec.ctypes.data_as(ctypes.c_void_p),
+                                        None) == 1
+    assert b"layer record 0" in lib.ic2_last_error()
+    # rows longer than the LDS-staged small GEMM holds
+    rec[0, :6] = 16
+    rec[0, 6:12] = [512, 600, 640, 64, 64, 1]
+    assert lib.ic2_modconv_prep_batched(ctypes.c_void_p(16), 512 * 16, 2, 512, 1, rec.ctypes.data_as(ctypes.c_void_p),
+                                        None) == 1
+    assert b"longer than 512" in lib.ic2_last_error()
+    # from_rgb: 5 input channels / a 96-wide output
+    f = ctypes.c_void_p(16)
+    assert nv.query("ic2_from_rgb_conv", f, 5, f, 32, f, f, 1, 8, 8, 32, None) == 1
+    assert b"cin" in lib.ic2_last_error()
+    assert nv.query("ic2_from_rgb_conv", f, 3, f, 32, f, f, 1, 8, 8, 96, None) == 1
+    # GroupNorm affine table: channels not divisible by the groups
+    assert nv.query("ic2_gn_affine_table", f, f, f, 2, 30, 32, 32, f, None) == 1
+    # GroupNorm-input conv: only where the 64-channel halo conv runs the shape
+    assert nv.query("ic2_conv3x3_gnin_supported", 1, 8, 256, 256, 64, 64, 3, 3, 1) == 1
+    assert nv.query("ic2_conv3x3_gnin_supported", 1, 8, 256, 256, 32, 64, 3, 3, 1) == 0
+    assert nv.query("ic2_conv3x3_gnin_supported", 0, 8, 256, 256, 64, 64, 3, 3, 1) == 0
+    assert nv.query("ic2_conv3x3_gnin_gn_fwd", f, None, 0.2, f, f, 1, 8, 256, 256, 64, 64, 64, 3, 3, 1, f, 32,
+                    1e-5, f, 1 << 20, None, 0, -1, None) == 1
+
+
 def test_product_path_refuses_cpu_tensors():
     with pytest.raises(RuntimeError, match="ROCm"):
         ic2.quantize_uniform(torch.zeros(4, 16, 512))
