@@ -1,18 +1,25 @@
 """Benchmark of the encode -> 8-bit quantize -> synthesize path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5] [--batch B] [--precision bf16|fp32]
-                    [--no-roofline] [--cpu-baseline-images M] [--dry-run]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2g|c2r|c4|c5] [--batch B]
+                    [--precision bf16|bf16-all|fp32] [--no-roofline] [--cpu-baseline-images M] [--dry-run]
 
 A step = one pass of the hot path over one synthetic batch already resident in HBM:
 HVAE_VGG_Encoder(img_resolution=1024) on 256^2 images -> 8-bit uniform quantizer (deterministic, means)
--> StyleGAN3-T synthesis -> uint8 PSNR sums vs the input -> all_reduce(SUM) of the fp64 metric record.
-Random-init weights of the named architectures (no checkpoints offline), seeded synthetic inputs
-(seed 1000 + rank).
+-> StyleGAN3-T synthesis -> uint8 PSNR sums vs the input + the code record (8-bit code histogram, index
+mismatches against the first step's codes) -> all_reduce(SUM) of the fp64 metric record.
+Random-init weights of the named architectures (no checkpoints offline), seeded synthetic inputs (seed 1000 + rank).
 
---config c5 (BASELINE config 5, the reference's train_hvae_encoder step, stylegan3_hvae_full.py:655-707): a step
-is one optimisation step of the encoder through the frozen synthesis network (forward, the reference's second
-encoder pass for the KL term, backward, data-parallel gradient all_reduce over RCCL, Adam); LPIPS excluded
-(its pretrained VGG weights are not available offline).
+--precision (encoder, synthesis): bf16 (default) = split-bf16 encoder ('bf16x3': three bf16 MFMA terms per
+product, f32 between layers -- the 8-bit indices of the fp32 reference, tests/test_gpu_c2_parity.py) + bf16
+synthesis; bf16-all = bf16 encoder + bf16 synthesis (round 2's mode: 4.6 % of the 8-bit indices differ from the
+reference's); fp32 = the exact-fp32 parity mode.
+
+--config c2g: the codebook path, GumbelSoftmaxCompressor.compress -> decompress (gumbel_softmax_compression.py:
+213-264) with the codes kept on the device (the reference's API moves them to the host; that PCIe round trip is
+not in the timed value).  --config c5 (BASELINE config 5, the reference's train_hvae_encoder step,
+stylegan3_hvae_full.py:655-707): one optimisation step of the encoder through the frozen synthesis network
+(forward, the reference's second encoder pass for the KL term, backward, data-parallel gradient all_reduce over
+RCCL, Adam); LPIPS excluded (its pretrained VGG weights are not available offline).
 
 Multi-GPU: one process per GPU, batch-sharded, weak scaling (every rank runs its own batch).  Under torchrun
 the ranks come from the env; `python bench.py --gpus N` without torchrun spawns the N ranks itself
@@ -28,7 +35,9 @@ pass after the headline loop, so the headline number carries no instrumentation.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
+import math
 import os
 import platform
 import statistics
@@ -45,6 +54,8 @@ from image_compression_2_amd import distributed as icd  # noqa: E402  (no GPU ac
 CONFIGS = {
     # name: (input res, generator res, per-GPU batch, description)
     "c2": (256, 256, 32, "batch=32 256x256 encode+8bit quantize+decode, SG3-T-256 generator"),
+    "c2g": (256, 256, 32, "batch=32 256x256 encode+8bit codebook quantize (GumbelSoftmaxCompressor.compress -> "
+                          "decompress, 256-entry codebook)+decode, SG3-T-256 generator"),
     "c4": (1024, 1024, 8, "batch=8 1024x1024 encode+8bit quantize+decode, SG3-T-1024 generator"),
     # reading (ii) of the 256^2 configs: the reference's default 1024 generator, its output bilinearly
     # decimated to the 256^2 input (StyleGAN3Compressor.forward, stylegan3_hvae_full.py:277-279)
@@ -52,9 +63,21 @@ CONFIGS = {
     "c5": (256, 256, 16, "HVAE encoder training step (rec MSE + 0.01 KL, Adam 1e-4) through frozen SG3-T-256, "
                          "256x256, per-GPU batch 16, grad all_reduce"),
 }
+# --precision -> (encoder precision, synthesis precision)
+PRECISIONS = {
+    "bf16": ("bf16x3", "bf16"),
+    "bf16-all": ("bf16", "bf16"),
+    "fp32": ("fp32", "fp32"),
+}
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA, MI355X_MICROARCH.md
 F32_PEAK_TFLOPS = 157.3     # f32 MFMA / VALU
 HBM_PEAK_GBS = 8000.0
+N_CODES = 256               # 8-bit codes: the record's histogram width
+
+CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gnin_gn_fwd", "ic2_from_rgb_conv",
+                "ic2_from_rgb_conv_x3")
+TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad",)
+FLR_ENTRIES = ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16")
 
 
 def parse(argv=None):
@@ -64,7 +87,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=sorted(PRECISIONS))
     ap.add_argument("--cpu-baseline-images", type=int, default=3, help="0 disables the CPU baseline leg")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU / gloo rehearsal of launcher + timing + reductions")
@@ -75,14 +98,16 @@ def parse(argv=None):
 # ------------------------------------------------------------------------------------------------
 # instrumentation (separate pass)
 class CallTimer:
-    """Brackets every libic2ops call whose name is in `names` with HIP events on the launching stream
-    (torch's current stream: every libic2ops kernel is enqueued there)."""
+    """Brackets every libic2ops call whose name is in `names` with HIP events on the launching stream (torch's
+    current stream: every libic2ops kernel is enqueued there).  Conv calls also carry the algorithmic FLOPs the
+    product code announced for them (_native.note_flops) and their arguments (-> the kernel the launch plan ran)."""
 
     def __init__(self, nv, names):
         self.nv = nv
         self.names = set(names)
-        self.events = {n: [] for n in names}
+        self.records = []      # (name, args, algorithmic flops | None, start event, end event)
         self.enabled = False
+        self.pending = None
         self._orig = None
 
     def install(self):
@@ -90,30 +115,61 @@ class CallTimer:
         self._orig = orig
 
         def call(name, *args):
+            f = None
+            if name in CONV_ENTRIES or name == "ic2_conv_wgrad":
+                f, timer.pending = timer.pending, None
             if not timer.enabled or name not in timer.names:
                 return orig(name, *args)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             rc = orig(name, *args)
             e.record()
-            timer.events[name].append((s, e))
+            timer.records.append((name, args, f, s, e))
             return rc
 
+        def hook(f):
+            timer.pending = f
+
         self.nv.call = call
+        self.nv._flops_hook = hook
 
     def uninstall(self):
         if self._orig is not None:
             self.nv.call = self._orig
+        self.nv._flops_hook = None
 
-    def total(self, names):
+    def calls(self, names):
+        """[(name, args, alg_flops, ms)] of the recorded calls named in `names`."""
         torch.cuda.synchronize()
-        ev = [p for n in names for p in self.events[n]]
-        return sum(s.elapsed_time(e) for s, e in ev), len(ev)
+        return [(n, a, f, s.elapsed_time(e)) for (n, a, f, s, e) in self.records if n in names]
+
+
+def conv_call_plan(nv, name, args):
+    """(kernel instance(s) the launch plan ran, MFMA FLOPs it executed incl. channel padding) of one conv call."""
+    if name in ("ic2_from_rgb_conv", "ic2_from_rgb_conv_x3"):
+        cin, (n, h, w, cout_p) = args[1], args[6:10]
+        return name[4:], 2 * n * h * w * cout_p * 9 * cin
+    if name == "ic2_conv_igemm_ws":
+        dt, odt, n, h, w, cin_p, cout_p, cv, kh, kw, pad = args[3:14]
+        layout = args[23]
+    elif name == "ic2_conv3x3_gn_fwd":
+        dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[3], args[4:13]
+        odt, layout = dt, nv.NHWC
+    elif name == "ic2_conv3x3_gnin_gn_fwd":
+        dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[5], args[6:15]
+        odt, layout = dt, nv.NHWC
+    elif name == "ic2_conv_wgrad":
+        dt, (n, h, w, cin_p, cout_p, kh, kw, pad) = args[3], args[4:12]
+        return "conv_wgrad", 2 * n * h * w * cout_p * kh * kw * cin_p
+    else:
+        raise KeyError(name)
+    ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
+    return nv.conv_plan(dt, odt, layout, n, h, w, cin_p, cout_p, cv, kh, kw, pad), 2 * n * ho * wo * cout_p * kh * kw * cin_p
 
 
 def algorithmic_flops_per_image(enc, G, res, split=False):
-    """MFMA-eligible FLOPs per image (unpadded): encoder convs + synthesis input 1x1 + modconvs
-    (split=True -> (encoder, synthesis))."""
+    """MFMA-eligible FLOPs per image (unpadded; the reference's convs): encoder convs + synthesis input 1x1 +
+    modconvs (split=True -> (encoder, synthesis))."""
     total = 0.0
     h = res
     total += 2 * h * h * enc.from_rgb.out_channels * 9 * enc.from_rgb.in_channels
@@ -150,7 +206,7 @@ def algorithmic_bytes_per_image(enc, G, res, esz):
     launch, not per image, and are added by the caller."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
     total, h = 0.0, res
-    total += h * h * (p32(enc.from_rgb.in_channels) + p32(enc.from_rgb.out_channels)) * esz
+    total += h * h * (enc.from_rgb.in_channels * 4 + p32(enc.from_rgb.out_channels) * esz)
     for blk in enc.blocks:
         if h <= 1:
             break
@@ -212,9 +268,10 @@ def pmc_traffic(config, precision, batch):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_traffic_{config}_{precision}_b{batch}.json")))
     if not files:
-        return None, None
+        return None
     rec = json.load(open(files[-1]))
-    return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    rec["src"] = os.path.relpath(files[-1], ROOT)
+    return rec
 
 
 def cpu_model():
@@ -227,11 +284,17 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(res, gen_res, n_images):
-    """The oracle (pure-PyTorch fp32 CPU restatement) timed on the host cores: encode + quantize + decode of
-    n_images, the fine fc1 drawn exactly as the reference re-creates it (nn.Linear(128, 256) default init,
-    stylegan3_hvae_full.py:225-230)."""
-    from oracle import encoder as oe
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may run on (the GPU box's CPU share), capped by
+    OMP_NUM_THREADS when set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def _oracle_setup(res, gen_res, n_images):
     from oracle import sg3
     import image_compression_2_amd as ic2
     torch.manual_seed(0)
@@ -241,21 +304,45 @@ def cpu_baseline(res, gen_res, n_images):
     x = torch.rand(n_images, 3, res, res, generator=torch.Generator().manual_seed(1000)) * 2 - 1
     torch.manual_seed(5)
     lin = torch.nn.Linear(128, 256)
-    fc1 = (lin.weight.detach(), lin.bias.detach())
+    return sd_e, sd_g, x, (lin.weight.detach(), lin.bias.detach())
+
+
+def cpu_baseline(res, gen_res, n_images, codebook=False):
+    """The oracle (pure-PyTorch fp32 CPU restatement) timed on the host cores: encode + quantize + decode of
+    n_images, the fine fc1 drawn exactly as the reference re-creates it (nn.Linear(128, 256) default init,
+    stylegan3_hvae_full.py:225-230).  codebook: the reference's GumbelSoftmaxCompressor quantizer (its full
+    discretization forward with Gumbel noise over [N*8192, 256], gumbel_softmax_compression.py:229) + lookup."""
+    from oracle import encoder as oe
+    from oracle import sg3
+    nt = cpu_threads()
+    torch.set_num_threads(nt)
+    sd_e, sd_g, x, fc1 = _oracle_setup(res, gen_res, n_images)
     t0 = time.perf_counter()
     with torch.no_grad():
         _, m, _ = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
-        q = oe.quantize_uniform(m, 8)
+        if codebook:
+            noise = oe.gumbel_noise(7, m.numel())
+            _, _, idx = oe.gumbel_forward(m, noise, 1.0, True)
+            q = oe.codebook_lookup(idx.reshape(m.shape))
+        else:
+            q = oe.quantize_uniform(m, 8)
         img = sg3.synthesis_forward(sd_g, gen_res, q)
         if img.shape[2] != res:
             torch.nn.functional.interpolate(img, size=(res, res), mode="bilinear", align_corners=False)
     dt = time.perf_counter() - t0
-    return dict(value=round(n_images / dt, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
-                cpu_model=cpu_model(),
-                sample=f"{n_images} image(s) {res}x{res}, encoder(1024-config) + 8-bit quantize + SG3-T-{gen_res} "
-                       f"{'(+ bilinear decimation) ' if gen_res != res else ''}"
-                       f"synthesis, fp32, oracle/ restatement on {torch.get_num_threads()} threads, {dt:.1f} s; "
-                       f"B=1 / B=32 / 1024^2 rows: profiles/r2_cpu_baseline.json")
+    out = dict(value=round(n_images / dt, 4), unit="images/s", cores=nt, kind="port", cpu_model=cpu_model(),
+               host_cpus=os.cpu_count(),
+               sample=f"{n_images} image(s) {res}x{res}, encoder(1024-config) + 8-bit "
+                      f"{'codebook (Gumbel forward + argmin + lookup)' if codebook else 'uniform'} quantize + "
+                      f"SG3-T-{gen_res} {'(+ bilinear decimation) ' if gen_res != res else ''}synthesis, fp32, "
+                      f"oracle/ restatement on {nt} threads, {dt:.1f} s")
+    if codebook:
+        # the quantizer alone at the reference's N=32 (SURVEY 6: 2.19 s on 8 Xeon cores)
+        z = torch.randn(32, 16, 512, generator=torch.Generator().manual_seed(3)) * 0.5
+        t0 = time.perf_counter()
+        oe.gumbel_forward(z, oe.gumbel_noise(8, z.numel()), 1.0, True)
+        out["quantizer_only_n32_s"] = round(time.perf_counter() - t0, 3)
+    return out
 
 
 def cpu_baseline_train(res, gen_res, n_images):
@@ -263,15 +350,10 @@ def cpu_baseline_train(res, gen_res, n_images):
     reference), synthesis forward, rec MSE + 0.01 KL, backward into the encoder's parameters."""
     from oracle import encoder as oe
     from oracle import sg3
-    import image_compression_2_amd as ic2
-    torch.manual_seed(0)
-    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024)
-    sd_e = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()}
-    sd_g = sg3.init_params(gen_res, seed=1)
-    x = torch.rand(n_images, 3, res, res, generator=torch.Generator().manual_seed(1000)) * 2 - 1
-    torch.manual_seed(5)
-    lin = torch.nn.Linear(128, 256)
-    fc1 = (lin.weight.detach(), lin.bias.detach())
+    nt = cpu_threads()
+    torch.set_num_threads(nt)
+    sd_e, sd_g, x, fc1 = _oracle_setup(res, gen_res, n_images)
+    sd_e = {k: v.clone().requires_grad_(True) for k, v in sd_e.items()}
     w_avg = torch.zeros(1, 1, 512)
     t0 = time.perf_counter()
     w, _, _ = oe.encoder_forward(sd_e, x, fine_fc1=fc1)
@@ -281,11 +363,10 @@ def cpu_baseline_train(res, gen_res, n_images):
     loss = torch.nn.functional.mse_loss(x, img) + 0.01 * kl
     loss.backward()
     dt = time.perf_counter() - t0
-    return dict(value=round(n_images / dt, 4), unit="images/s", cores=torch.get_num_threads(), kind="port",
-                cpu_model=cpu_model(),
+    return dict(value=round(n_images / dt, 4), unit="images/s", cores=nt, kind="port", cpu_model=cpu_model(),
+                host_cpus=os.cpu_count(),
                 sample=f"{n_images} image(s) {res}x{res}: encoder(1024-config) fwd x2 + SG3-T-{gen_res} synthesis fwd "
-                       f"+ MSE/KL + backward, fp32 autograd over the oracle/ restatement on {torch.get_num_threads()} "
-                       f"threads, {dt:.1f} s")
+                       f"+ MSE/KL + backward, fp32 autograd over the oracle/ restatement on {nt} threads, {dt:.1f} s")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -317,6 +398,18 @@ def timed_loop(step, steps, sync, barrier, use_events):
     return out, elapsed, per
 
 
+def record_summary(vec, n_codes=N_CODES):
+    """The all-reduced metric record [sse, pixels, images, index mismatches vs the first step, codes out of
+    range, hist[n_codes]] -> reported fields (global over ranks)."""
+    hist = vec[5:5 + n_codes].double()
+    total = float(hist.sum()) + float(vec[4])
+    p = hist / max(total, 1.0)
+    perplexity = float(torch.exp(-torch.sum(p * torch.log(p + 1e-10))))
+    return {"psnr_db_vs_input": None, "codes": int(round(total)), "index_mismatch_vs_first_step": int(vec[3]),
+            "codes_out_of_range": int(vec[4]), "code_perplexity": round(perplexity, 3),
+            "hist_nonzero_bins": int((hist > 0).sum())}
+
+
 def run(args):
     dry = args.dry_run
     rank, world, local = icd.init("gloo" if dry else None)
@@ -324,6 +417,7 @@ def run(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     res, gen_res, batch, desc = CONFIGS[args.config]
     batch = args.batch or batch
+    enc_prec, syn_prec = PRECISIONS[args.precision]
     if dry:
         dev = torch.device("cpu")
         sync = lambda: None
@@ -334,14 +428,18 @@ def run(args):
     barrier = lambda: icd.barrier(dev)
 
     if dry:
-        # stand-in step: the same seeded per-rank batch, a metric record and its all_reduce
+        # stand-in step: the same seeded per-rank batch, a metric record (SSE, counts, 8-bit code histogram of
+        # the image itself) and its all_reduce
         g = torch.Generator().manual_seed(1000 + rank)
         x = torch.rand(batch, 3, 16, 16, generator=g) * 2 - 1
         from oracle import metrics as om
+        from oracle import encoder as oe
+        codes = oe.uniform_indices(x, 8).reshape(-1)
 
         def step():
             sse = float(om.sse_uint8(x, x.flip(0)).sum())
-            vec = torch.tensor([sse, float(x.numel()), float(batch)], dtype=torch.float64)
+            hist = torch.bincount(codes.clamp(0, N_CODES - 1), minlength=N_CODES).double()
+            vec = torch.cat([torch.tensor([sse, float(x.numel()), float(batch), 0.0, 0.0], dtype=torch.float64), hist])
             return icd.allreduce_sum(vec)
         enc = G = comp = nv = None
     else:
@@ -350,17 +448,22 @@ def run(args):
         from image_compression_2_amd import metrics as icm
         train = args.config == "c5"
         torch.manual_seed(0)
-        enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=args.precision).to(dev)
+        enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=syn_prec if train else enc_prec).to(dev)
         if not train:
             enc.eval().requires_grad_(False)
         torch.manual_seed(1)
-        G = ic2.Generator(img_resolution=gen_res, precision=args.precision).to(dev).eval()
-        comp = ic2.StyleGAN3Compressor(enc, G, training_resolution=res if train else None)
+        G = ic2.Generator(img_resolution=gen_res, precision=syn_prec).to(dev).eval()
+        if args.config == "c2g":
+            comp = ic2.GumbelSoftmaxCompressor(enc, G).to(dev)
+        else:
+            comp = ic2.StyleGAN3Compressor(enc, G, training_resolution=res if train else None)
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         x = torch.rand(batch, 3, res, res, generator=g, device=dev) * 2 - 1
         # (pixel count, image count) of the metric record: device constants made once, so the step has no
         # host->device copy (a pageable one stalls the host until the stream drains)
         counts = torch.tensor([float(x.numel()), float(batch)], dtype=torch.float64, device=dev)
+        stream = nv.stream_of(x)
+        golden = {}
 
         if train:
             from image_compression_2_amd import training as ict
@@ -373,14 +476,30 @@ def run(args):
                                  (losses["kl_loss"].double() * batch).view(1), counts[1:]])
                 return icd.allreduce_sum(vec, device=dev)
 
+        def code_record(codes, kind):
+            """[index mismatches vs the first step's codes, out-of-range codes, hist[256]] (ic2_code_record)."""
+            rec = torch.zeros(N_CODES + 2, dtype=torch.int32, device=dev)
+            if "codes" not in golden:
+                golden["codes"] = codes.clone()
+            gold = golden["codes"]
+            nv.call("ic2_code_record", nv.ptr(codes), kind, N_CODES, 8 if kind == 0 else 0, nv.ptr(gold),
+                    codes.numel(), nv.ptr(rec), stream)
+            return torch.cat([rec[N_CODES + 1:], rec[N_CODES:N_CODES + 1], rec[:N_CODES]]).double()
+
         def step():
             with torch.no_grad():
-                q = comp.compress(x, quantization_bits=8, deterministic=True)
-                img = comp.decompress(q)
+                if args.config == "c2g":
+                    codes = comp.compress_codes(x, discrete_bits=8)
+                    img = comp.decompress(codes)
+                    rec = code_record(codes, 1)
+                else:
+                    q = comp.compress(x, quantization_bits=8, deterministic=True)
+                    img = comp.decompress(q)
+                    rec = code_record(q, 0)
                 if img.shape[2] != res:
                     img = ic2.resize_bilinear(img, (res, res))
                 sse = icm.uint8_sse(img, x)
-            vec = torch.cat([sse.sum().view(1), counts])
+            vec = torch.cat([sse.sum().view(1), counts, rec])
             return icd.allreduce_sum(vec, device=dev)
 
     if not dry and args.config == "c5":
@@ -398,6 +517,7 @@ def run(args):
     value = total_images / elapsed_max
     vec = vec.cpu()
     metric = {"c2": "images/sec encode+decode 256px", "c4": "images/sec encode+decode 1024px",
+              "c2g": "images/sec encode+codebook quantize+decode 256px",
               "c2r": "images/sec encode+decode 256px (1024 generator, decimated)",
               "c5": "images/sec encoder training step 256px"}[args.config]
     out = {
@@ -411,12 +531,13 @@ def run(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.precision,
+        "dtype": "bf16" if args.precision != "fp32" else "fp32",
         "data": "synthetic (seeded uniform [-1,1] images resident in HBM, seed 1000+rank; random-init encoder + "
                 "SG3-T weights)",
         "config": {"workload": desc, "global_batch": batch * world, "per_gpu_batch": batch, "resolution": res,
                    "generator": f"stylegan3-t-{gen_res} (random init)", "encoder": "HVAE_VGG_Encoder(img_resolution=1024)",
-                   "quantization_bits": 8, "parallelism": f"dp{world} (batch-sharded, RCCL metric all_reduce)"},
+                   "quantization_bits": 8, "parallelism": f"dp{world} (batch-sharded, RCCL metric all_reduce)",
+                   "precision": {"encoder": enc_prec if args.config != "c5" else syn_prec, "synthesis": syn_prec}},
         "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
         "ms_per_step_median": round(median_max, 3),
         "per_rank_ms_per_step": per_rank_ms,
@@ -425,6 +546,8 @@ def run(args):
     if dry:
         out["dry_run"] = True
         out["psnr_db_record"] = float(10 * torch.log10(255.0 ** 2 / (vec[0] / vec[1])))
+        out["metric_record"] = record_summary(vec)
+        out["metric_record"]["hist_sum"] = int(vec[5:].sum())
     elif args.config == "c5":
         out["config"].update(quantization_bits=None, loss="rec MSE + 0.01 KL(w_avg); LPIPS excluded (no weights "
                              "offline)", optimizer="Adam(1e-4, (0.9, 0.999))",
@@ -434,75 +557,23 @@ def run(args):
     else:
         from image_compression_2_amd import metrics as icm
         out["psnr_db_vs_input"] = round(icm.psnr_from_sums(vec[0].item(), vec[1].item()), 4)
+        rs = record_summary(vec)
+        rs.pop("psnr_db_vs_input")
+        out["metric_record"] = rs
+        if args.config == "c2g":
+            out["config"]["quantizer"] = "GumbelSoftmaxCompressor (linspace(-1,1,256) codebook, exact argmin)"
 
-    if not dry and not args.no_roofline and args.config == "c5":
-        names = ("ic2_conv_igemm", "ic2_conv_igemm_ws", "ic2_conv_wgrad")
-        timer = CallTimer(nv, names)
-        timer.install()
-        timer.enabled = True
-        n_inst = min(args.steps, 5)
-        timed_loop(step, n_inst, sync, barrier, use_events=True)
-        timer.enabled = False
-        timer.uninstall()
-        conv_ms, n_launch = timer.total(names)
-        flops_img = training_flops_per_image(enc, G, res)
-        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
-        achieved = flops_img * batch * n_inst / (conv_ms * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": "ic2 conv family forward + dgrad (implicit GEMM) + wgrad",
-                           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(achieved / peak, 4), "traffic": None, "launches": n_launch,
-                           "avg_launch_ms": round(conv_ms / max(n_launch, 1), 4),
-                           "conv_ms_per_step": round(conv_ms / n_inst, 3),
-                           "path_frac": round(value / world * flops_img / (peak * 1e12), 4),
-                           "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}
-    elif not dry and not args.no_roofline:
-        conv_names = ("ic2_conv_igemm", "ic2_conv_igemm_ws")
-        timer = CallTimer(nv, conv_names + ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16"))
-        timer.install()
-        timer.enabled = True
-        n_inst = min(args.steps, 10)
-        timed_loop(step, n_inst, sync, barrier, use_events=True)
-        timer.enabled = False
-        timer.uninstall()
-        conv_ms, n_launch = timer.total(conv_names)
-        flr_ms, n_flr = timer.total(("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16"))
-        flops_img = algorithmic_flops_per_image(enc, G, res)
-        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
-        traffic, traffic_src = pmc_traffic(args.config, args.precision, batch)
-        esz = 2 if args.precision == "bf16" else 4
-        wb, n_conv = weight_bytes(enc, G, res, esz)
-        alg_bytes = (algorithmic_bytes_per_image(enc, G, res, esz) * batch + wb) / n_conv
-        achieved = flops_img * batch * n_inst / (conv_ms * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": "ic2 conv family (igemm / halo conv / ToRGB, every "
-                                                      "encoder conv, synthesis input 1x1 and modulated conv)",
-                           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                           "traffic_src": traffic_src, "algorithmic_bytes_per_launch": round(alg_bytes),
-                           "launches": n_launch, "avg_launch_ms": round(conv_ms / max(n_launch, 1), 4),
-                           "conv_ms_per_step": round(conv_ms / n_inst, 3),
-                           "path_frac": round(value / world * flops_img / (peak * 1e12), 4),
-                           "algorithmic_gflop_per_image": round(flops_img / 1e9, 2)}
-        if args.precision == "bf16" and n_flr:
-            f_img, b_img, bound_img = flr_work_per_image(G)
-            flr_step = flr_ms / n_inst
-            bound_step = bound_img * batch * 1e3
-            out["roofline"]["flr"] = {
-                "kernel": "ic2 flrelu_mfma (fused filtered lrelu, every synthesis layer but ToRGB)",
-                "bound": "valu (FIR on f32 VALU, SURVEY.md 8(d)); the kernel itself runs the FIR on f16 MFMA",
-                "fir_gflop_per_image": round(f_img / 1e9, 3), "bytes_per_image": round(b_img),
-                "ms_per_step": round(flr_step, 3), "bound_ms_per_step": round(bound_step, 3),
-                "frac_of_bound": round(bound_step / flr_step, 4),
-                "achieved_tflops": round(f_img * batch / (flr_step * 1e-3) / 1e12, 2),
-                "achieved_gbs": round(b_img * batch / (flr_step * 1e-3) / 1e9, 1), "launches": n_flr}
+    if not dry and not args.no_roofline:
+        out["roofline"] = roofline(args, nv, step, sync, barrier, enc, G, res, batch, value / world, enc_prec,
+                                   syn_prec)
 
-    if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry and args.config == "c5":
-        out["cpu_baseline"] = cpu_baseline_train(res, gen_res, 1)
-    elif rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
-        if args.config == "c2r":
+    if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
+        if args.config == "c5":
+            out["cpu_baseline"] = cpu_baseline_train(res, gen_res, 1)
+        elif args.config in ("c2r", "c4"):
             out["cpu_baseline"] = cpu_baseline(res, gen_res, 1)
         else:
-            out["cpu_baseline"] = cpu_baseline(res if args.config == "c2" else 256,
-                                               gen_res if args.config == "c2" else 256, args.cpu_baseline_images)
+            out["cpu_baseline"] = cpu_baseline(res, gen_res, args.cpu_baseline_images, codebook=args.config == "c2g")
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -511,6 +582,93 @@ def run(args):
                 f.write(line + "\n")
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def roofline(args, nv, step, sync, barrier, enc, G, res, batch, img_s_per_gpu, enc_prec, syn_prec):
+    """The instrumented pass: every conv entry point (and every filtered lrelu) bracketed by HIP events.
+      conv family: algorithmic FLOPs announced by the product per launch (the reference's conv FLOPs) / the summed
+                   time of every conv launch -> achieved, frac of the dense bf16 peak;
+      dominant:    the kernel instance with the largest share of that time (launch plan, ic2_conv_plan): its
+                   launches' algorithmic and executed (padded-channel) MFMA FLOPs / their time;
+      flr:         the fused filtered lrelu against its FIR-on-VALU bound and its HBM floor."""
+    train = args.config == "c5"
+    conv_names = TRAIN_CONV_ENTRIES if train else CONV_ENTRIES
+    timer = CallTimer(nv, conv_names + FLR_ENTRIES)
+    timer.install()
+    timer.enabled = True
+    n_inst = min(args.steps, 5 if train else 10)
+    try:
+        timed_loop(step, n_inst, sync, barrier, use_events=True)
+    finally:
+        timer.enabled = False
+        timer.uninstall()
+    conv_calls = timer.calls(conv_names)
+    conv_ms = sum(c[3] for c in conv_calls)
+    peak = BF16_PEAK_TFLOPS if args.precision != "fp32" else F32_PEAK_TFLOPS
+    per = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # plan -> calls, ms, alg flops, executed flops
+    for name, a, f, ms in conv_calls:
+        plan, exe = conv_call_plan(nv, name, a)
+        r = per[plan]
+        r[0] += 1
+        r[1] += ms
+        r[2] += f or 0.0
+        r[3] += exe
+    if train:
+        alg = training_flops_per_image(enc, G, res) * batch * n_inst
+        kernel = "ic2 conv family forward + dgrad (implicit GEMM) + wgrad"
+    else:
+        alg = sum(f for _, _, f, _ in conv_calls if f)
+        missing = [n for n, _, f, _ in conv_calls if f is None]
+        assert not missing, f"conv calls without announced FLOPs: {set(missing)}"
+        kernel = ("ic2 conv family: every conv entry point of the step (from_rgb, encoder convs, synthesis input 1x1, "
+                  "modulated convs, ToRGB)")
+    achieved = alg / (conv_ms * 1e-3) / 1e12
+    dom_plan, d = max(per.items(), key=lambda kv: kv[1][1])
+    rl = {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+          "frac": round(achieved / peak, 4), "traffic": None, "launches": len(conv_calls),
+          "avg_launch_ms": round(conv_ms / max(len(conv_calls), 1), 4), "conv_ms_per_step": round(conv_ms / n_inst, 3),
+          "algorithmic_gflop_per_image": round(alg / (batch * n_inst) / 1e9, 2),
+          "executed_gflop_per_image": round(sum(r[3] for r in per.values()) / (batch * n_inst) / 1e9, 2),
+          "path_frac": round(img_s_per_gpu * alg / (batch * n_inst) / (peak * 1e12), 4),
+          "precision": {"encoder": enc_prec, "synthesis": syn_prec}}
+    rl["dominant"] = {"kernel": dom_plan, "launches_per_step": round(d[0] / n_inst, 2),
+                      "ms_per_step": round(d[1] / n_inst, 3), "avg_launch_ms": round(d[1] / d[0], 4),
+                      "algorithmic_gflop_per_launch": round(d[2] / d[0] / 1e9, 3) if d[2] else None,
+                      "achieved": round(d[2] / (d[1] * 1e-3) / 1e12, 2) if d[2] else None,
+                      "executed_achieved": round(d[3] / (d[1] * 1e-3) / 1e12, 2),
+                      "frac": round(d[2] / (d[1] * 1e-3) / 1e12 / peak, 4) if d[2] else None,
+                      "executed_frac": round(d[3] / (d[1] * 1e-3) / 1e12 / peak, 4)}
+    rl["per_kernel"] = {k: {"launches_per_step": round(v[0] / n_inst, 2), "ms_per_step": round(v[1] / n_inst, 3),
+                            "alg_tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[2] else None,
+                            "executed_tflops": round(v[3] / (v[1] * 1e-3) / 1e12, 1)}
+                        for k, v in sorted(per.items(), key=lambda kv: -kv[1][1])}
+    if not train:
+        esz = 2 if args.precision != "fp32" else 4
+        wb, n_conv = weight_bytes(enc, G, res, esz)
+        rl["algorithmic_bytes_per_launch"] = round((algorithmic_bytes_per_image(enc, G, res, esz) * batch + wb) / n_conv)
+        pm = pmc_traffic(args.config, args.precision, batch)
+        if pm is not None:
+            rl["traffic"] = pm["hbm_bytes_per_launch"]
+            rl["traffic_unit"] = "bytes/launch"
+            rl["traffic_src"] = pm["src"]
+    flr_calls = timer.calls(FLR_ENTRIES)
+    if syn_prec == "bf16" and flr_calls and not train:
+        flr_ms = sum(c[3] for c in flr_calls)
+        f_img, b_img, bound_img = flr_work_per_image(G)
+        flr_step = flr_ms / n_inst
+        hbm_floor = b_img * batch / (HBM_PEAK_GBS * 1e9) * 1e3
+        rl["flr"] = {
+            "kernel": "ic2 flrelu_mfma (fused filtered lrelu, every synthesis layer but ToRGB)",
+            "bound": "hbm (the kernel runs its FIRs on f16 MFMA, so its floor is the compulsory bytes at 8 TB/s); "
+                     "bound_ms_per_step = SURVEY 8(d)'s FIR-on-f32-VALU bound, for comparison",
+            "fir_gflop_per_image": round(f_img / 1e9, 3), "bytes_per_image": round(b_img),
+            "ms_per_step": round(flr_step, 3), "hbm_floor_ms_per_step": round(hbm_floor, 3),
+            "frac_of_hbm_floor": round(hbm_floor / flr_step, 4),
+            "achieved_gbs": round(b_img * batch / (flr_step * 1e-3) / 1e9, 1),
+            "bound_ms_per_step": round(bound_img * batch * 1e3, 3),
+            "frac_of_bound": round(bound_img * batch * 1e3 / flr_step, 4),
+            "achieved_tflops": round(f_img * batch / (flr_step * 1e-3) / 1e12, 2), "launches": len(flr_calls)}
+    return rl
 
 
 def main(argv=None):

@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libic2ops.so")
 
-F32, BF16, F16 = 0, 1, 2
+F32, BF16, F16, BF16X3 = 0, 1, 2, 3
 ACT_LINEAR, ACT_LRELU = 0, 1
 NHWC, NCHW, NHWC16 = 0, 1, 2
 
@@ -26,9 +26,12 @@ _F = ctypes.c_float
 # name -> argtypes (restype int unless listed in _RESTYPE)
 _SIGS = {
     "ic2_abi_version": [],
+    "ic2_dev_mode": [],
+    "ic2_conv_plan": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_quantize_uniform": [_P, _I64, _I, _P, _P, _P],
     "ic2_quantize_codebook_argmin": [_P, _I64, _P, _I, _P, _P, _P, _P],
     "ic2_codebook_lookup": [_P, _I64, _P, _I, _P, _P, _P],
+    "ic2_code_record": [_P, _I, _I, _I, _P, _I64, _P, _P],
     "ic2_gumbel_softmax_quantize": [_P, _I64, _P, _I, _P, _F, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
                                     _P],
     "ic2_bias_act": [_P, _P, _P, _I, _I64, _I64, _I64, _I, _F, _F, _F, _P],
@@ -51,6 +54,7 @@ _SIGS = {
     "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "ic2_from_rgb_conv": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
+    "ic2_from_rgb_conv_x3": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "ic2_nhwc_to_nchw": [_P, _I, _P, _I, _I, _I, _I, _I, _P],
     "ic2_group_norm_stats_floats": [_I, _I, _I],
     "ic2_group_norm_stats": [_P, _I, _I, _I, _I, _I, _I, _F, _P, _P],
@@ -85,7 +89,7 @@ _SIGS = {
     "ic2_flrelu_bwd_nhwc": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F,
                             _F, _I, _P],
 }
-_RESTYPE = {"ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
+_RESTYPE = {"ic2_conv_plan": ctypes.c_char_p, "ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
             "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64, "ic2_conv_wgrad_ws_floats": _I64,
             "ic2_gn_lrelu_pool_bwd_floats": _I64, "ic2_conv3x3_gn_stats_floats": _I64,
             "ic2_flrelu_bwd_ydot_floats": _I64, "ic2_scale_bwd_part_floats": _I64}
@@ -138,6 +142,12 @@ def query(name, *args):
     return getattr(load(), name)(*args)
 
 
+def conv_plan(dtype, out_dtype, out_layout, n, h, w, cin_p, cout_p, cout_valid, kh, kw, pad):
+    """Name of the kernel instance(s) ic2_conv_igemm_ws launches for this geometry (the library's launch plan)."""
+    return query("ic2_conv_plan", dtype, out_dtype, out_layout, n, h, w, cin_p, cout_p, cout_valid, kh, kw,
+                 pad).decode()
+
+
 def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo, oscale, bias,
                act, slope, act_gain, clamp, out_mul, out_layout, stream, device):
     """ic2_conv_igemm with the split-K workspace the launch plan asks for (a stream-ordered torch
@@ -146,6 +156,25 @@ def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, k
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=device) if nbytes > 0 else None
     return call("ic2_conv_igemm_ws", x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho,
                 wo, oscale, bias, act, slope, act_gain, clamp, out_mul, out_layout, ptr(ws), nbytes, stream)
+
+
+_flops_hook = None   # installed by bench.py's instrumented pass: receives each conv's algorithmic FLOPs
+
+
+def note_flops(alg_flops):
+    """Announce the algorithmic (unpadded, reference) FLOPs of the conv launch that follows (accounting for the
+    benchmark's per-call roofline; a no-op unless an instrumented pass installed a hook)."""
+    if _flops_hook is not None:
+        _flops_hook(alg_flops)
+
+
+def knob(name, default):
+    """Development knob (the native library's rule, errors.hip): the environment variable `name` is read only when
+    IC2_DEV=1, so the default launch plan never depends on the process environment."""
+    if os.environ.get("IC2_DEV") != "1":
+        return default
+    v = os.environ.get(name)
+    return default if v is None else type(default)(v)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -166,20 +195,44 @@ class AutogradUnsupported(RuntimeError):
     pass
 
 
-def forbid_autograd(what, tensors=(), modules=()):
-    """The HIP forwards return tensors without a grad_fn.  Where the reference caller would train through
-    them (stylegan3_hvae_full.py:669-696: the encoder's loss backpropagates through the frozen generator into
-    W+), a silent result would run and learn nothing, so refuse instead: raise when grad mode is on and any
-    input or parameter requires grad."""
+def grad_inputs(tensors=(), modules=()):
+    """The tensors / parameters a graph would have to reach: [] unless grad mode is on."""
     if not torch.is_grad_enabled():
-        return
-    need = any(t is not None and t.requires_grad for t in tensors)
-    need = need or any(p.requires_grad for m in modules for p in m.parameters())
-    if need:
+        return []
+    req = [t for t in tensors if isinstance(t, torch.Tensor) and t.requires_grad]
+    return req + [p for m in modules for p in m.parameters() if p.requires_grad]
+
+
+class _RefuseBackward(torch.autograd.Function):
+    """Graph node for HIP forwards without a backward: the forward result is returned as is (no copy); a
+    backward through it raises instead of silently producing no gradient."""
+
+    @staticmethod
+    def forward(ctx, what, n_out, *args):
+        ctx.what = what
+        return tuple(a.detach() for a in args[:n_out])
+
+    @staticmethod
+    def backward(ctx, *grads):
         raise AutogradUnsupported(
-            f"{what}: autograd through the HIP path is not implemented for this module (training, SURVEY.md "
-            "8(f) #3).  Run inference under torch.no_grad() / torch.inference_mode(), or freeze the module with "
-            ".requires_grad_(False)")
+            f"{ctx.what}: backward through the HIP path is not implemented for this module (training, SURVEY.md "
+            "8(f) #3; the reference trains only the encoder, through a frozen generator).  Freeze the module with "
+            ".requires_grad_(False) or detach its inputs")
+
+
+def refuse_backward(what, outputs, tensors=(), modules=()):
+    """Return `outputs` (a tensor or a tuple) unchanged when no graph is wanted; otherwise attached to a node whose
+    backward raises AutogradUnsupported (inference in grad mode keeps working; only .backward() fails)."""
+    req = grad_inputs(tensors, modules)
+    if not req:
+        return outputs
+    single = isinstance(outputs, torch.Tensor)
+    outs = [outputs] if single else list(outputs)
+    fl = [i for i, o in enumerate(outs) if isinstance(o, torch.Tensor) and o.is_floating_point()]
+    wrapped = _RefuseBackward.apply(what, len(fl), *[outs[i] for i in fl], *req)
+    for k, i in enumerate(fl):
+        outs[i] = wrapped[k]
+    return outs[0] if single else tuple(outs)
 
 
 def ptr(t):
@@ -207,6 +260,19 @@ def torch_dtype(precision):
     if precision in ("bf16", torch.bfloat16):
         return torch.bfloat16
     raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+
+
+ENCODER_PRECISIONS = ("fp32", "bf16", "bf16x3")
+
+
+def encoder_dtype(precision):
+    """HVAE_VGG_Encoder precision -> (activation storage dtype, split).  'bf16x3' = split bf16 (ic2ops.h
+    IC2_BF16X3): bf16 MFMA operands [hi | hi | lo] x [hi | lo | hi], f32 conv outputs, GroupNorm in f32."""
+    if precision == "bf16x3":
+        return torch.bfloat16, True
+    if precision in ENCODER_PRECISIONS:
+        return torch_dtype(precision), False
+    raise ValueError(f"encoder precision must be one of {ENCODER_PRECISIONS}, got {precision!r}")
 
 
 def pad32(c):

@@ -14,6 +14,9 @@ namespace ic2 {
 // ------------------------------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 
+// development knob `name` (integer env var), read only when IC2_DEV=1, else `dflt` (errors.hip)
+int knob(const char* name, int dflt);
+
 #define IC2_CHECK_ARG(cond, ...)                      \
   do {                                                \
     if (!(cond)) {                                    \

@@ -3,6 +3,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace ic2 {
 
@@ -13,6 +14,15 @@ static int grid_1d(int64_t total, int per = 1) {
   return (int)g;
 }
 
+// Split-bf16 activations (ic2ops.h IC2_BF16X3): logical channel stride c_p stored as 3 * c_p bf16 channels
+// [hi | hi | lo] per pixel, hi = bf16(v), lo = bf16(v - hi) (v - hi is exact in f32).
+struct bf16x3_t {
+  bf16_t v;
+};
+__device__ __forceinline__ void split_bf16(float v, bf16_t& hi, bf16_t& lo) {
+  hi = f2bf(v);
+  lo = f2bf(v - bf2f(hi));
+}
 // ------------------------------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int n,
@@ -26,6 +36,25 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restri
     float v = ch < c ? x[(nn * c + ch) * hw + p] : 0.f;
     if (scale) v *= scale[nn * c_p + ch];
     st(y + e, v);
+  }
+}
+
+__global__ void __launch_bounds__(256) nchw_to_nhwc_x3_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int n,
+                                                              int c, int hw, int c_p, const float* __restrict__ scale) {
+  const int64_t total = (int64_t)n * hw * c_p;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(e % c_p);
+    const int64_t pix = e / c_p;
+    const int p = (int)(pix % hw);
+    const int64_t nn = pix / hw;
+    float v = ch < c ? x[(nn * c + ch) * hw + p] : 0.f;
+    if (scale) v *= scale[nn * c_p + ch];
+    bf16_t hi, lo;
+    split_bf16(v, hi, lo);
+    bf16_t* o = y + pix * 3 * c_p + ch;
+    o[0] = hi;
+    o[c_p] = hi;
+    o[2 * c_p] = lo;
   }
 }
 
@@ -178,6 +207,29 @@ template <> __device__ __forceinline__ void st8<bf16_t>(bf16_t* p, const float (
   *reinterpret_cast<uint4*>(p) = u;
 }
 
+// eight consecutive channels ch0 .. ch0+7 of pixel `pix` (tensor-global pixel index) with logical stride c_p
+template <typename T>
+__device__ __forceinline__ void st8p(T* out, int64_t pix, int c_p, int ch0, const float (&v)[8]) {
+  st8(out + pix * c_p + ch0, v);
+}
+template <>
+__device__ __forceinline__ void st8p<bf16x3_t>(bf16x3_t* out, int64_t pix, int c_p, int ch0, const float (&v)[8]) {
+  bf16_t* b = reinterpret_cast<bf16_t*>(out) + pix * 3 * c_p + ch0;
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bf16_t h0, l0, h1, l1;
+    split_bf16(v[2 * k], h0, l0);
+    split_bf16(v[2 * k + 1], h1, l1);
+    h[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    l[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+  }
+  const uint4 hv = make_uint4(h[0], h[1], h[2], h[3]);
+  *reinterpret_cast<uint4*>(b) = hv;
+  *reinterpret_cast<uint4*>(b + c_p) = hv;
+  *reinterpret_cast<uint4*>(b + 2 * c_p) = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y, TO* __restrict__ out, int n, int h,
                                                        int w, int c_p, int c, int groups,
@@ -232,7 +284,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const TI* __restrict__ y,
     } else {
       f(oy, ox, res, false);
     }
-    st8(out + pix * c_p + ch0, res);
+    st8p(out, pix, c_p, ch0, res);
   }
 }
 
@@ -270,7 +322,6 @@ __global__ void __launch_bounds__(256) gn_apply_oct_kernel(const TI* __restrict_
     }
   }
   const TI* yb = y + (int64_t)nn * h * w * c_p + ch0;
-  TO* ob = out + (int64_t)nn * ohw * c_p + ch0;
   for (int pix = blockIdx.x * ppi + prow; pix < ohw; pix += gridDim.x * ppi) {
     float res[8];
     auto f = [&](int idx, bool accum) {
@@ -295,7 +346,7 @@ __global__ void __launch_bounds__(256) gn_apply_oct_kernel(const TI* __restrict_
     } else {
       f(pix, false);
     }
-    st8(ob + (int64_t)pix * c_p, res);
+    st8p(out, (int64_t)nn * ohw + pix, c_p, ch0, res);
   }
 }
 
@@ -313,7 +364,15 @@ __global__ void __launch_bounds__(256) gap_partial_kernel(const T* __restrict__ 
   if (ch >= c_p) return;
   const int p0 = chunk * GAP_CHUNK, p1 = min(hw, p0 + GAP_CHUNK);
   float s = 0.f;
-  for (int p = p0; p < p1; ++p) s += ld(x + ((int64_t)nn * hw + p) * c_p + ch);
+  if constexpr (std::is_same<T, bf16x3_t>::value) {
+    const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
+    for (int p = p0; p < p1; ++p) {
+      const bf16_t* px = xb + ((int64_t)nn * hw + p) * 3 * c_p + ch;
+      s += bf2f(px[0]) + bf2f(px[2 * c_p]);
+    }
+  } else {
+    for (int p = p0; p < p1; ++p) s += ld(x + ((int64_t)nn * hw + p) * c_p + ch);
+  }
   part[((int64_t)nn * nchunks + chunk) * c_p + ch] = s;
 }
 
@@ -448,6 +507,9 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, x, (bf16_t*)y, n, c, h * w,
                        c_p, scale);
+  else if (dtype == IC2_BF16X3)
+    hipLaunchKernelGGL(nchw_to_nhwc_x3_kernel, dim3(grid_1d(total)), dim3(256), 0, s, x, (bf16_t*)y, n, c, h * w, c_p,
+                       scale);
   else
     IC2_CHECK_ARG(false, "nchw_to_nhwc: bad dtype");
   IC2_CHECK_LAUNCH("nchw_to_nhwc");
@@ -462,8 +524,10 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
 // thread computes one pixel's COUT outputs with packed FMAs against the bf16 weights held in LDS (broadcast
 // reads).  Arithmetic: bf16 operands, f32 sums (tap order), + bias, one bf16 rounding -- as the MFMA conv.
 // ------------------------------------------------------------------------------------------------
-template <int COUT>
-__global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const bf16_t* __restrict__ wp,
+// X3 (the encoder's split-bf16 mode, ic2_from_rgb_conv_x3): wp is the nn.Conv2d weight itself (f32 [cout][cin][3][3],
+// `cin_p` = cout there), the image is not rounded, and the f32 result is stored split ([hi | hi | lo], 3 * COUT).
+template <int COUT, bool X3 = false>
+__global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const void* __restrict__ wp,
                                                        int cin_p, const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                        int h, int w, int tiles_x, int tiles_y) {
   constexpr int TH = 8, TW = 32, HH = TH + 2, HW = TW + 2;
@@ -480,14 +544,20 @@ __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__
   for (int e = t; e < nk * COUT; e += 256) {
     const int o = e % COUT, k = e / COUT;
     const int tap = k / cin, c = k - (k / cin) * cin;
-    wl[k][o] = bf2f(wp[((int64_t)o * 9 + tap) * cin_p + c]);
+    if constexpr (X3)
+      wl[k][o] = o < cin_p ? reinterpret_cast<const float*>(wp)[((int64_t)o * cin + c) * 9 + tap] : 0.f;
+    else
+      wl[k][o] = bf2f(reinterpret_cast<const bf16_t*>(wp)[((int64_t)o * 9 + tap) * cin_p + c]);
   }
   for (int e = t; e < cin * HH * HW; e += 256) {
     const int c = e / (HH * HW), r = e - c * (HH * HW);
     const int yy = r / HW, xx = r - (r / HW) * HW;
     const int iy = oy0 - 1 + yy, ix = ox0 - 1 + xx;
     float v = 0.f;
-    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) v = bf2f(f2bf(x[(((int64_t)nn * cin + c) * h + iy) * w + ix]));
+    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) {
+      v = x[(((int64_t)nn * cin + c) * h + iy) * w + ix];
+      if constexpr (!X3) v = bf2f(f2bf(v));
+    }
     xin[c][yy][xx] = v;
   }
   __syncthreads();
@@ -512,6 +582,27 @@ __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__
   }
   const int oy = oy0 + py, ox = ox0 + px;
   if (oy >= h || ox >= w) return;
+  if constexpr (X3) {
+    bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * 3 * COUT;
+#pragma unroll
+    for (int q = 0; q < COUT / 8; ++q) {
+      uint32_t hw_[4], lw_[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = 8 * q + 2 * k;
+        bf16_t h0, l0, h1, l1;
+        split_bf16(acc[o / 2].x + bias[o], h0, l0);
+        split_bf16(acc[o / 2].y + bias[o + 1], h1, l1);
+        hw_[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        lw_[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+      }
+      const uint4 hv = make_uint4(hw_[0], hw_[1], hw_[2], hw_[3]);
+      reinterpret_cast<uint4*>(yo)[q] = hv;
+      reinterpret_cast<uint4*>(yo + COUT)[q] = hv;
+      reinterpret_cast<uint4*>(yo + 2 * COUT)[q] = make_uint4(lw_[0], lw_[1], lw_[2], lw_[3]);
+    }
+    return;
+  }
   bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * COUT;
 #pragma unroll
   for (int q = 0; q < COUT / 8; ++q) {
@@ -538,12 +629,36 @@ extern "C" int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin
   IC2_CHECK_ARG(blocks < (1LL << 31), "from_rgb_conv: too many tiles");
   hipStream_t s = as_stream(stream);
   if (cout_p == 32)
-    hipLaunchKernelGGL(from_rgb_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, (const bf16_t*)w, cin_p, bias,
+    hipLaunchKernelGGL(from_rgb_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cin_p, bias,
                        (bf16_t*)y, h, w_, tiles_x, tiles_y);
   else
-    hipLaunchKernelGGL(from_rgb_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, (const bf16_t*)w, cin_p, bias,
+    hipLaunchKernelGGL(from_rgb_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cin_p, bias,
                        (bf16_t*)y, h, w_, tiles_x, tiles_y);
   IC2_CHECK_LAUNCH("from_rgb_conv");
+  return IC2_OK;
+}
+
+extern "C" int ic2_from_rgb_conv_x3(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n,
+                                    int h, int w_, int cout_p, void* stream) {
+  IC2_CHECK_ARG(x && w && bias && y && n > 0 && h > 0 && w_ > 0, "from_rgb_conv_x3: null pointer / bad geometry");
+  IC2_CHECK_ARG(cin >= 1 && cin <= 4 && cout >= 1 && cout <= cout_p && (cout_p == 32 || cout_p == 64 || cout_p == 128),
+                "from_rgb_conv_x3: needs 1 <= cin <= 4, cout <= cout_p, cout_p in {32, 64, 128} (cin=%d cout=%d cout_p=%d)",
+                cin, cout, cout_p);
+  IC2_CHECK_ARG((uintptr_t)y % 16 == 0, "from_rgb_conv_x3: output must be 16-byte aligned");
+  const int tiles_x = (w_ + 31) / 32, tiles_y = (h + 7) / 8;
+  const int64_t blocks = (int64_t)n * tiles_x * tiles_y;
+  IC2_CHECK_ARG(blocks < (1LL << 31), "from_rgb_conv_x3: too many tiles");
+  hipStream_t s = as_stream(stream);
+  if (cout_p == 32)
+    hipLaunchKernelGGL((from_rgb_kernel<32, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  else if (cout_p == 64)
+    hipLaunchKernelGGL((from_rgb_kernel<64, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL((from_rgb_kernel<128, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  IC2_CHECK_LAUNCH("from_rgb_conv_x3");
   return IC2_OK;
 }
 
@@ -715,6 +830,7 @@ extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dty
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(bf16_t, bf16_t);
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_F32) IC2_GN_LAUNCH(bf16_t, float);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(float, bf16_t);
+  else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16X3) IC2_GN_LAUNCH(float, bf16x3_t);
   else IC2_CHECK_ARG(false, "gn_lrelu_pool: bad dtypes");
 #undef IC2_GN_LAUNCH
   IC2_CHECK_LAUNCH("gn_lrelu_pool");
@@ -735,6 +851,8 @@ extern "C" int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int 
     hipLaunchKernelGGL(gap_partial_kernel<float>, grid, dim3(256), 0, s, (const float*)x, hw, c_p, nchunks, part);
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(gap_partial_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, hw, c_p, nchunks, part);
+  else if (dtype == IC2_BF16X3)
+    hipLaunchKernelGGL(gap_partial_kernel<bf16x3_t>, grid, dim3(256), 0, s, (const bf16x3_t*)x, hw, c_p, nchunks, part);
   else
     IC2_CHECK_ARG(false, "global_avg_pool: bad dtype");
   hipLaunchKernelGGL(gap_finalize_kernel, dim3((unsigned)ceil_div((int64_t)n * c, 256)), dim3(256), 0, s, part, n, c_p,

@@ -248,8 +248,7 @@ static const FlrGeomSel kFlrGeoms[] = {
 constexpr int kNumFlrGeoms = sizeof(kFlrGeoms) / sizeof(kFlrGeoms[0]);
 static int flr_variant() {
   static const int v = [] {
-    const char* e = getenv("IC2_FLR_VARIANT");
-    const int x = e ? atoi(e) : -1;
+    const int x = knob("IC2_FLR_VARIANT", -1);
     return (x >= 0 && x < kNumFlrGeoms) ? x : -1;
   }();
   return v;
@@ -346,11 +345,8 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   a.py0 = py0; a.px0 = px0;
   hipStream_t s = as_stream(stream);
   // bf16 NHWC (the synthesis throughput path): the MFMA formulation (flrelu_mfma.hip) unless
-  // IC2_FLR_MFMA=0 asks for the VALU kernel below
-  static const bool use_mfma = [] {
-    const char* e = getenv("IC2_FLR_MFMA");
-    return !(e && e[0] == '0');
-  }();
+  // knob IC2_FLR_MFMA=0 asks for the VALU kernel below
+  static const bool use_mfma = knob("IC2_FLR_MFMA", 1) != 0;
   // f16 input (the synthesis conv epilogue's output) exists only for the MFMA formulation
   // (one polyphase phase for both axes: the instances take a single delta)
   const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) && dtype_out == IC2_BF16 && b == nullptr &&

@@ -332,11 +332,8 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
   const int q = px0 - fu_taps + 1 - fd_taps + 1;
   const int ph = ((-q) % down + down) % down;
   const int R = fd_taps - 1 - ph;
-  // tile variants (TIY, TIX, channel pairs, threads); IC2_FLRB_VARIANT=k picks one (tuning, tools/bench_flr_bwd.py)
-  static const int variant = [] {
-    const char* e = getenv("IC2_FLRB_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
+  // tile variants (TIY, TIX, channel pairs, threads); knob IC2_FLRB_VARIANT=k picks one (tuning, tools/bench_flr_bwd.py)
+  static const int variant = knob("IC2_FLRB_VARIANT", -1);
   const int v = variant >= 0 ? variant : 1;   // 16x16 tiles: fastest on every SG3-T-256 layer (profiles/r2_flr_bwd_variants.txt)
   int tiy, tix, np;
   if (v == 1) { tiy = 16; tix = 16; np = cfg2 ? 2 : 1; }

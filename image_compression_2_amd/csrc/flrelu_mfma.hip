@@ -795,11 +795,8 @@ static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
   a.tiles_x = (int)ceil_div(a.out_w, TOX);
   a.tiles_y = (int)ceil_div(a.out_h, 16);
   a.cblocks = a.c_p / 16;
-  // IC2_FLR_ORDER=1: spatial tiles fastest, so the tiles one XCD runs together share their input halos in its L2
-  static const int order = [] {
-    const char* e = getenv("IC2_FLR_ORDER");
-    return e ? atoi(e) : 0;
-  }();
+  // knob IC2_FLR_ORDER=1: spatial tiles fastest, so the tiles one XCD runs together share their input halos in its L2
+  static const int order = knob("IC2_FLR_ORDER", 0);
   a.order = order;
   const int ntiles = n * a.tiles_y * a.tiles_x * a.cblocks;
   static int resident = 0;
@@ -815,34 +812,12 @@ static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
 }
 
 // the clamp-split activation needs a finite clamp whose reciprocal scaling keeps the f16 operands normal
-// (lim in [2^-4, 2^12]: SG3's conv_clamp 256 / sqrt(2)); IC2_FLR_CLSPLIT=0 keeps the 3-instruction activation
+// (lim in [2^-4, 2^12]: SG3's conv_clamp 256 / sqrt(2)); knob IC2_FLR_CLSPLIT=0 keeps the 3-instruction activation.
+// (The kernel's ABL template parameter held the round-2 ablation builds; only ABL = 0 is instantiated.)
 template <int U, int DELTA>
 static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
-  static const bool split = [] {
-    const char* e = getenv("IC2_FLR_CLSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  // IC2_FLR_ABL (diagnostic, gives WRONG results): bit 1 drops the in-tile barriers, 2 the activation VALU, 4 the
-  // input DMA, 8 the output stores, 64 blocked output addressing, 16 the horizontal phase, 32 the vertical-down phase; only for the (2, 1) and (4, 2) geometries
-  static const int abl = [] {
-    const char* e = getenv("IC2_FLR_ABL");
-    return e ? atoi(e) : 0;
-  }();
+  static const bool split = knob("IC2_FLR_CLSPLIT", 1) != 0;
   if (split && a.lim >= 0.0625f && a.lim <= 4096.f) {
-    if constexpr ((U == 2 && DELTA == 1) || (U == 4 && DELTA == 2)) {
-      switch (abl) {
-        case 1: fm2_launch_cl<U, DELTA, true, 1>(a, n, s); return;
-        case 2: fm2_launch_cl<U, DELTA, true, 2>(a, n, s); return;
-        case 4: fm2_launch_cl<U, DELTA, true, 4>(a, n, s); return;
-        case 8: fm2_launch_cl<U, DELTA, true, 8>(a, n, s); return;
-        case 12: fm2_launch_cl<U, DELTA, true, 12>(a, n, s); return;
-        case 64: fm2_launch_cl<U, DELTA, true, 64>(a, n, s); return;
-        case 16: fm2_launch_cl<U, DELTA, true, 16>(a, n, s); return;
-        case 32: fm2_launch_cl<U, DELTA, true, 32>(a, n, s); return;
-        case 7: fm2_launch_cl<U, DELTA, true, 7>(a, n, s); return;
-        default: break;
-      }
-    }
     fm2_launch_cl<U, DELTA, true, 0>(a, n, s);
   } else {
     fm2_launch_cl<U, DELTA, false, 0>(a, n, s);
@@ -866,26 +841,12 @@ static void fm_launch_alias(const FlrArgs& a, int ntiles, hipStream_t s) {
                      ntiles);
 }
 
-// IC2_FLR_ALIAS=0/1 selects the separate-V/D (3 workgroups per CU, default) or the aliased (4 per CU) LDS
-// layout for up 2; up 4 (30.5 KB) already fits 5 workgroups and keeps the separate layout.  Measured on the
-// bench (batch 32): 1180 vs 1185 img/s -- the extra barriers cancel the occupancy gain, so the kernel is
-// not occupancy-bound.
+// The separate-V/D LDS layout on 4 waves.  Measured and not kept (round 2): the aliased layout (4 workgroups per
+// CU instead of 3; 1180 vs 1185 img/s -- the extra barriers cancel the occupancy gain) and the same tile on 8 waves
+// (FLR 9.0 vs 8.1 ms per C2 step: the kernel wants independent MFMA chains per wave more than it wants waves).
 template <int U, int DELTA, bool IN_F16>
 static void fm_launch_one(const FlrArgs& a, int ntiles, hipStream_t s) {
-  static const int alias = [] {
-    const char* e = getenv("IC2_FLR_ALIAS");
-    return e ? atoi(e) : 0;
-  }();
-  // IC2_FLR_WAVES=8: the same tile on 8 waves (half the rows / columns per wave, 90 VGPRs, 2 workgroups =
-  // 16 waves per CU instead of 12).  Measured slower (FLR 9.0 vs 8.1 ms per C2 step): the kernel wants
-  // independent MFMA chains per wave between barriers more than it wants waves.
-  static const int waves = [] {
-    const char* e = getenv("IC2_FLR_WAVES");
-    return e && atoi(e) == 8 ? 8 : 4;
-  }();
-  if (U == 2 && alias) fm_launch_alias<U, DELTA, IN_F16, true, 4>(a, ntiles, s);
-  else if (waves == 8) fm_launch_alias<U, DELTA, IN_F16, false, 8>(a, ntiles, s);
-  else fm_launch_alias<U, DELTA, IN_F16, false, 4>(a, ntiles, s);
+  fm_launch_alias<U, DELTA, IN_F16, false, 4>(a, ntiles, s);
 }
 
 template <bool IN_F16>
@@ -909,11 +870,8 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
   if ((int64_t)a.in_h * a.in_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // 32-bit buffer offsets
   if (a.xsc != 1 || a.xsx % 8 != 0) return IC2_E_UNSUPPORTED;  // 16-B chunks of 8 channels
   if ((int64_t)a.out_h * a.out_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // output offsets too
-  // the wide (16 x 32) tile for the f16-input synthesis path unless IC2_FLR_WIDE=0
-  static const bool wide = [] {
-    const char* e = getenv("IC2_FLR_WIDE");
-    return !(e && e[0] == '0');
-  }();
+  // the wide (16 x 32) tile for the f16-input synthesis path unless knob IC2_FLR_WIDE=0
+  static const bool wide = knob("IC2_FLR_WIDE", 1) != 0;
   // (only where 32-column tiles pad the output no wider than 16-column ones: not the 36-wide SG3 layers)
   if (in_f16 && wide && ceil_div(a.out_w, 32) * 32 <= ceil_div(a.out_w, 16) * 16 &&
       (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {

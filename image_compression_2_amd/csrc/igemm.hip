@@ -677,268 +677,15 @@ static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1
 }
 
 // ------------------------------------------------------------------------------------------------
-// Halo implicit GEMM for the wide 3x3 layers (bf16, cin_p % 64 == 0): the modulated convs of SG3 synthesis
-// and the encoder's wide blocks.  The implicit GEMM above stages a shifted 256-pixel panel per tap, so every
-// input pixel crosses L2 -> LDS nine times per 64-channel block; here the output tile is a 2-D block of
-// TH x TW = 256 pixels of one sample, and its (TH+2) x (TW+2) input halo is staged ONCE per 64-channel block
-// (1.27-1.33x the pixels instead of 9x) and read at nine shifted offsets from LDS.  Only the weight slab
-// (BO output channels x one tap x 64 channels) is streamed per K-step.
-//   bytes per 64-channel block per tile: 9 x BO x 128 B (weights) + halo  -> 229 FLOP/B at BO 256 vs 128
-// 8 waves, each owning 128 output channels x (256 OG / 8) pixels: OG = 2: 2 o-groups x 4 p-groups (64 px);
-// OG = 1: 8 p-groups of 32 px.  LDS: 2 weight slabs (ring) + 2 halos (the next block's halo lands by LDS-DMA
-// behind the current block's 9 taps), rows of 128 B with the 16-B chunk XOR swizzle of the 8-phase kernels.
-// K-step t = (block cb = t / 9, tap = t % 9): barrier; fragment reads; DMA of step t+1's weight slab (and at
-// tap 0 of the next block's halo); 64 (OG 2) / 32 (OG 1) MFMAs per wave; vmcnt(0).
-// Output channel rows wholly in the padding (cout_p 192 / 384 tails) skip their MFMAs.
-static bool ig_env_off(const char* name);
-
-template <int OG, int TW>
-struct HG {
-  static constexpr int BO = 128 * OG, TH = 256 / TW;
-  static constexpr int HW = TW + 2, HH = TH + 2, NH = HH * HW;  // halo pixels
-  static constexpr int NHI = (NH + 7) / 8;                      // 1-KiB DMA instructions per halo (8 px each)
-  static constexpr int HPW = (NHI + 7) / 8;                     // per wave, at most
-  static constexpr int HALO_B = NHI * 1024;
-  static constexpr int WS_B = BO * 128;                         // one weight slab: BO rows x 64 channels
-  static constexpr int NWI = BO / 64;                           // weight DMA instructions per wave
-  static constexpr int J = 2 * OG;                              // 16-pixel blocks per wave
-  static constexpr int LDS_B = 2 * WS_B + 2 * HALO_B;
-};
-
-template <int OG, int TW>
-__device__ __forceinline__ void hgemm_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
-  using G = HG<OG, TW>;
-  constexpr int J = G::J, NWI = G::NWI, HPW = G::HPW;
-  __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
-  char* const wsl = lds;                    // 2 weight slabs
-  char* const hal = lds + 2 * G::WS_B;      // 2 halos
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int og = OG == 2 ? wid >> 2 : 0;
-  const int pg = OG == 2 ? wid & 3 : wid;
-  const int fr = lane & 15, fh = lane >> 4;
-
-  // tile: o fastest (the o-tiles of one pixel tile share its halo in L2), XCD-aware
-  const int logical = xcd_remap(blockIdx.x, a.nblocks);
-  const int o_tile = logical % a.tiles_o;
-  int pt = logical / a.tiles_o;
-  const int tx = pt % tiles_x;
-  pt /= tiles_x;
-  const int ty = pt % tiles_y;
-  const int nn = pt / tiles_y;
-  const int o0 = o_tile * G::BO;
-  const int oy0 = ty * G::TH, ox0 = tx * TW;
-
-  const char* __restrict__ xg = reinterpret_cast<const char*>(a.x);
-  const char* __restrict__ wg = reinterpret_cast<const char*>(a.w);
-  const int lrow = lane >> 3, pch = lane & 7;
-
-  // weight DMA: instruction k of this wave fills slab rows (wid + 8k) * 8 + lrow; per-lane offset is constant
-  // across K-steps (the step's (tap, block) part is the descriptor base)
-  uint32_t w_off[NWI];
-#pragma unroll
-  for (int k = 0; k < NWI; ++k) {
-    const int row = (wid + 8 * k) * 8 + lrow;
-    const int o = o0 + row;
-    w_off[k] = o < a.cout_p ? (uint32_t)(o * a.K * 2 + ((pch ^ ((row >> 1) & 7)) << 4)) : kOob;
-  }
-  // halo DMA: instruction g = wid + 8k moves halo pixels g*8 .. g*8+7; offset of the pixel's 64-channel
-  // block 0 (the block index is in the descriptor base); outside the image / past the halo -> kOob (zeros)
-  uint32_t h_off[HPW];
-#pragma unroll
-  for (int k = 0; k < HPW; ++k) {
-    const int g = wid + 8 * k;
-    const int hp = g * 8 + lrow;
-    const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
-    const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
-    const bool ok = g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
-    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ ((hp >> 1) & 7)) << 3)) * 2) : kOob;
-  }
-  // B fragment rows: pixel block pb = pg * J + j -> tile pixel (py, px0 + fr); halo row at tap (0, 0)
-  int brow[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int pb = pg * J + j;
-    const int py = pb * 16 / TW, px = (pb * 16) % TW + fr;
-    brow[j] = py * G::HW + px;
-  }
-  const int obase = og * 128;
-  const bool live0 = o0 + obase < a.cout_p, live1 = o0 + obase + 64 < a.cout_p;
-  const int CB = a.cin_p >> 6;
-  const int nq = CB * 9;
-
-  auto issue_w = [&](int t) {  // weight slab of K-step t -> slab t & 1
-    const int cb = t / 9, tap = t - (t / 9) * 9;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(wg + ((int64_t)tap * a.cin_p + cb * 64) * 2), 0, t < nq ? kOob : 0, kRsrcWord3);
-    char* dst = wsl + (t & 1) * G::WS_B;
-#pragma unroll
-    for (int k = 0; k < NWI; ++k)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
-                                               16, w_off[k], 0, 0, 0);
-  };
-  auto issue_h = [&](int cb) {  // halo of block cb -> halo cb & 1
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 128), 0, kOob, kRsrcWord3);
-    char* dst = hal + (cb & 1) * G::HALO_B;
-#pragma unroll
-    for (int k = 0; k < HPW; ++k)
-      if (wid + 8 * k < G::NHI)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 8 * k) * 1024),
-                                                 16, h_off[k], 0, 0, 0);
-  };
-
-  f32x4 acc[8][J];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue_h(0);
-  issue_w(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (int t = 0; t < nq; ++t) {
-    __builtin_amdgcn_s_barrier();  // step t's slab and block t/9's halo landed for every wave; step t-1 read
-    __builtin_amdgcn_sched_barrier(0);
-    const int cb = t / 9, tap = t - (t / 9) * 9;
-    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-    const char* wl = wsl + (t & 1) * G::WS_B;
-    const char* hl = hal + (cb & 1) * G::HALO_B;
-    bf16x8 af[8][2], bfr[J][2];
-    if (live0) {
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int row = brow[j] + ky * G::HW + kx;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) bfr[j][s] = *reinterpret_cast<const bf16x8*>(hl + g8_off(row, 4 * s + fh));
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) af[i][s] = *reinterpret_cast<const bf16x8*>(wl + g8_off(obase + i * 16 + fr, 4 * s + fh));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < nq) issue_w(t + 1);               // slab (t+1) & 1 was read by step t-1 (before the barrier)
-    if (tap == 0 && cb + 1 < CB) issue_h(cb + 1);  // halo (cb+1) & 1 was read by block cb-1
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    if (live0) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
-    }
-    if (live1) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 4; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for step t+1 landed
-  }
-
-  // epilogue: lane holds C[o = o0 + obase + 16 i + 4 fh + r][tile pixel (pb, fr)]
-  const int hw = a.ho * a.wo;
-  float4 sc[8], bi[8];  // one sample per tile: every channel block's operands before the first store
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    sc[i] = ig_load_oscale(a, nn, o0 + obase + i * 16 + 4 * fh);
-    bi[i] = ig_load_bias(a, o0 + obase + i * 16 + 4 * fh);
-  }
-  ig_preloads_done();
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int pb = pg * J + j;
-    const int oy = oy0 + pb * 16 / TW, ox = ox0 + (pb * 16) % TW + fr;
-    if (oy >= a.ho || ox >= a.wo) continue;
-    const int pix = oy * a.wo + ox;
-    const int p = nn * hw + pix;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int ob = o0 + obase + i * 16 + 4 * fh;
-      if (ob >= a.cout_p) continue;
-      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
-    }
-  }
-}
-
-// one non-template kernel per instance (a __global__ template's host stub is not emitted here)
-__global__ void __launch_bounds__(512, 1) hgemm_o2_w32_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<2, 32>(a, tx, ty); }
-__global__ void __launch_bounds__(512, 1) hgemm_o2_w16_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<2, 16>(a, tx, ty); }
-__global__ void __launch_bounds__(512, 1) hgemm_o1_w32_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<1, 32>(a, tx, ty); }
-__global__ void __launch_bounds__(512, 1) hgemm_o1_w16_kernel(IgemmArgs a, int tx, int ty) { hgemm_body<1, 16>(a, tx, ty); }
-
-template <int OG, int TW>
-static void launch_hgemm(IgemmArgs a, hipStream_t s) {
-  using G = HG<OG, TW>;
-  const int tiles_x = (int)ceil_div(a.wo, TW), tiles_y = (int)ceil_div(a.ho, G::TH);
-  a.tiles_o = (a.cout_p + G::BO - 1) / G::BO;
-  a.nblocks = a.n * tiles_x * tiles_y * a.tiles_o;
-  const dim3 grid(a.nblocks), block(512);
-  if (OG == 2 && TW == 32) hipLaunchKernelGGL(hgemm_o2_w32_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
-  else if (OG == 2) hipLaunchKernelGGL(hgemm_o2_w16_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
-  else if (TW == 32) hipLaunchKernelGGL(hgemm_o1_w32_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
-  else hipLaunchKernelGGL(hgemm_o1_w16_kernel, grid, block, 0, s, a, tiles_x, tiles_y);
-}
-
-// instance choice: pixel tile 16 x 16 or 8 x 32, whichever pads the output less; 256 output channels per
-// workgroup when cout_p is a multiple of 256 (or 192: one o-tile, its last 64 rows skipped), else 128
-struct HgPlan {
-  bool tw32, og2;
-  int64_t blocks;
-};
-static HgPlan hg_plan(int n, int ho, int wo, int cout_p) {
-  const int64_t a16 = ceil_div(ho, 16) * 16 * ceil_div(wo, 16) * 16;
-  const int64_t a32 = ceil_div(ho, 8) * 8 * ceil_div(wo, 32) * 32;
-  HgPlan p;
-  p.tw32 = a32 <= a16;
-  p.og2 = cout_p % 256 == 0 || cout_p == 192;
-  const int64_t tiles = p.tw32 ? ceil_div(ho, 8) * ceil_div(wo, 32) : ceil_div(ho, 16) * ceil_div(wo, 16);
-  p.blocks = n * tiles * ceil_div(cout_p, p.og2 ? 256 : 128);
-  return p;
-}
-
-// bf16 3x3 with 64-deep channel blocks whose buffer offsets fit 31 bits, on a grid of >= ~1 workgroup per CU
-// (smaller launches keep the split-K implicit GEMM).  Measured against the 8-phase implicit GEMM on the bench
-// shapes (profiles/r2_hgemm_sweep.txt): faster on the encoder's 128^2 / 64^2 blocks and on SG3 L12 (192 -> 128
-// at 276^2), level on L11 / L13, slower on the 512-wide layers (there the 8-phase kernel's staggered halves
-// keep the matrix pipe busier than the halo saves) and wherever the 2-D tiles pad the image by > 5 %.
-// So: cin_p, cout_p <= 256 and >= 95 % tile utilisation.  IC2_HGEMM=0 disables it, =2 forces it wherever legal.
-static bool hgemm_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
-  static const int mode = [] {
-    // default off since the channel-major K order (round 2f): the 8-phase kernel then matches or beats it on the
-    // 256-wide encoder blocks it used to win (e2b 1062 vs 1133 TF/s), and hg4 took the <= 192-wide layers
-    const char* e = getenv("IC2_HGEMM");
-    return e ? atoi(e) : 0;
-  }();
-  if (!(mode && dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 64 == 0 && cout_p % 64 == 0 &&
-        x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))
-    return false;
-  const HgPlan p = hg_plan(n, ho, wo, cout_p);
-  if (p.blocks < 240) return false;
-  if (mode == 2) return true;
-  const double util = (double)ho * wo * n * ceil_div(cout_p, p.og2 ? 256 : 128) / (256.0 * p.blocks);
-  return cin_p <= 256 && cout_p <= 256 && util >= 0.95;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Halo implicit GEMM, 4-wave form (`hg4`): the same halo idea as hgemm above, shaped for two workgroups per CU.
-// hgemm runs ONE 8-wave workgroup per CU whose waves all meet at the per-K-step barrier, so the two waves of a
-// SIMD read their fragments at the same time and then compete for the matrix pipe at the same time (MFMA busy
-// 0.30-0.38 on the 128 / 192-wide SG3 layers, profiles/r2_pmc_shapes_c2_bf16_b32.json).  Here a workgroup is
-// 4 waves (one per SIMD) and needs <= 74 KB of LDS, so two independent workgroups share each CU and one's
-// barrier / fragment-read phase overlaps the other's MFMAs without any ping-pong bookkeeping.
+// Halo implicit GEMM, 4-wave form (`hg4`).  The implicit GEMM above stages a shifted pixel panel per tap, so every
+// input pixel crosses L2 -> LDS nine times per channel block; here the output tile is a 2-D block of pixels of one
+// sample whose (TH+2) x (TW+2) input halo is staged ONCE per 32-channel block and read at nine shifted offsets.
+// An 8-wave form of the same idea (one workgroup per CU, all waves meeting at each K-step barrier: MFMA busy
+// 0.30-0.38, round 2) was removed; here a workgroup is 4 waves (one per SIMD) and needs <= 74 KB of LDS, so two
+// independent workgroups share each CU and one's barrier / fragment-read phase overlaps the other's MFMAs.
 //   K-step = one tap x 32 channels (64-B LDS rows); wave tile (16 I) o x (16 J) px, 2 fragments per MFMA pair
 //   read per step: I + J ds_read_b128 for I*J MFMAs (8 + 4 for 32 at the 128 x 256 tile: 12 KB per wave and
-//   step, 40 % less LDS read traffic per MFMA than hgemm's 128 x 32 wave tile at 64 channels).
+//   step).
 //   Weights stream through a 3-slab ring (the slab for step t+2 is issued at step t, so a DMA has a whole step
 //   plus the barrier to land); the next 32-channel block's halo is spread over the first taps of the current
 //   block, one 1-KiB DMA per wave per step, so every step waits for the same small count (vmcnt(NWI [+1])).
@@ -1143,40 +890,28 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
                                                                                           int ty) {            \
     hg4_body<I, J, WGO, WGP, TW, NS, true>(a, tx, ty);                                                           \
   }
-IC2_HG4_KERNEL(hg4_o128_w32_kernel, 8, 4, 1, 4, 32, 3)    // 128 o x (8 x 32) px
-IC2_HG4_KERNEL(hg4_o128_w16_kernel, 8, 4, 1, 4, 16, 3)    // 128 o x (16 x 16) px
-IC2_HG4_KERNEL(hg4_o192_w32_kernel, 6, 4, 2, 2, 32, 3)    // 192 o x (4 x 32) px
-IC2_HG4_KERNEL(hg4_o192_w16_kernel, 6, 4, 2, 2, 16, 3)    // 192 o x (8 x 16) px
-IC2_HG4_KERNEL(hg4_o256_w32_kernel, 8, 4, 2, 2, 32, 3)    // 256 o x (4 x 32) px
-IC2_HG4_KERNEL(hg4_o256_w16_kernel, 8, 4, 2, 2, 16, 3)    // 256 o x (8 x 16) px
-IC2_HG4_KERNEL(hg4_o128_w32_s4_kernel, 8, 4, 1, 4, 32, 4) // 4-slab weight ring (three K-steps ahead)
-IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)
-IC2_HG4_KERNEL(hg4_o192_w32_s4_kernel, 6, 4, 2, 2, 32, 4)
-IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)
-IC2_HG4_KERNEL(hg4_o64_w32_s4_kernel, 4, 4, 1, 4, 32, 4)   // 64 o x (8 x 32) px: the 64-wide layers
-IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)
-IC2_HG4_KERNEL_HB(hg4_o128_w32_hb_kernel, 8, 4, 1, 4, 32, 4)
-IC2_HG4_KERNEL_HB(hg4_o192_w32_hb_kernel, 6, 4, 2, 2, 32, 4)
-IC2_HG4_KERNEL_HB(hg4_o64_w32_hb_kernel, 4, 4, 1, 4, 32, 4)
+// the launch plan's instances: halo-burst (HB) kernels for 32-wide pixel tiles, 4-slab rings for 16-wide ones
+IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)  // 128 o x (16 x 16) px
+IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)  // 192 o x (8 x 16) px
+IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)   // 64 o x (16 x 16) px
+IC2_HG4_KERNEL_HB(hg4_o128_w32_hb_kernel, 8, 4, 1, 4, 32, 4)  // 128 o x (8 x 32) px
+IC2_HG4_KERNEL_HB(hg4_o192_w32_hb_kernel, 6, 4, 2, 2, 32, 4)  // 192 o x (4 x 32) px
+IC2_HG4_KERNEL_HB(hg4_o64_w32_hb_kernel, 4, 4, 1, 4, 32, 4)   // 64 o x (8 x 32) px
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_HB
 
-static int hg4_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// instance: o-tile 256 when cout_p % 256 == 0, 192 when cout_p % 192 == 0, else 128 (IC2_HG4_BO=128 forces 128);
-// pixel tile 32 or 16 wide, whichever pads the output less
+// instance: o-tile 192 when cout_p % 192 == 0, 128 when cout_p % 128 == 0, else 64 (IC2_HG4_BO=128 forces 128 where
+// it divides); pixel tile 32 or 16 wide, whichever pads the output less
 struct H4Plan {
   int bo;
   bool tw32;
   int64_t blocks;
 };
 static H4Plan h4_plan(int n, int ho, int wo, int cout_p) {
-  static const int force_bo = hg4_env("IC2_HG4_BO", 0);
+  static const int force_bo = knob("IC2_HG4_BO", 0);
   H4Plan p;
-  p.bo = force_bo == 128 ? 128 : cout_p % 256 == 0 ? 256 : cout_p % 192 == 0 ? 192 : cout_p % 128 == 0 ? 128 : 64;
+  p.bo = cout_p % 192 == 0 ? 192 : cout_p % 128 == 0 ? 128 : 64;
+  if (force_bo == 128 && cout_p % 128 == 0) p.bo = 128;
   const int bp = p.bo <= 128 ? 256 : 128;
   const int th32 = bp / 32, th16 = bp / 16;
   const int64_t a32 = ceil_div(ho, th32) * th32 * ceil_div(wo, 32) * 32;
@@ -1196,92 +931,55 @@ static void launch_hg4(IgemmArgs a, hipStream_t s, void (*kern)(IgemmArgs, int, 
   hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(256), 0, s, a, tiles_x, tiles_y);
 }
 
+// the halo burst on 32-wide tiles (s276a +2.6 %, s276b +3 %, SG3-T-1024 L11 +7 % over spreading the halo DMAs over
+// the first taps, profiles/r2f_hg4_hb.txt); a 4-slab weight ring (+0.5-1 % over 3, profiles/r2e_hg4_sweep.txt)
 static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
-  static const int ns = hg4_env("IC2_HG4_NS", 4);  // 4-slab ring: +0.5-1 % over 3 (profiles/r2e_hg4_sweep.txt)
-  static const int hb = hg4_env("IC2_HG4_HB", 1);  // halo burst: s276a +2.6 %, s276b +3 %, T11 +7 % (profiles/r2f_hg4_hb.txt)
   const H4Plan p = h4_plan(a.n, a.ho, a.wo, a.cout_p);
-  if (hb && ns == 4 && p.tw32 && p.bo != 256) {
+  if (p.tw32) {
     if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, hg4_o192_w32_hb_kernel);
     else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_hb_kernel);
     else launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_hb_kernel);
-    return;
-  }
-  if (p.bo == 256) {
-    if (p.tw32) launch_hg4<8, 4, 2, 2, 32>(a, s, hg4_o256_w32_kernel);
-    else launch_hg4<8, 4, 2, 2, 16>(a, s, hg4_o256_w16_kernel);
-  } else if (p.bo == 192) {
-    if (p.tw32) launch_hg4<6, 4, 2, 2, 32>(a, s, ns == 4 ? hg4_o192_w32_s4_kernel : hg4_o192_w32_kernel);
-    else launch_hg4<6, 4, 2, 2, 16>(a, s, ns == 4 ? hg4_o192_w16_s4_kernel : hg4_o192_w16_kernel);
-  } else if (p.bo == 128) {
-    if (p.tw32) launch_hg4<8, 4, 1, 4, 32>(a, s, ns == 4 ? hg4_o128_w32_s4_kernel : hg4_o128_w32_kernel);
-    else launch_hg4<8, 4, 1, 4, 16>(a, s, ns == 4 ? hg4_o128_w16_s4_kernel : hg4_o128_w16_kernel);
   } else {
-    if (p.tw32) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_s4_kernel);
+    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 16>(a, s, hg4_o192_w16_s4_kernel);
+    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 16>(a, s, hg4_o128_w16_s4_kernel);
     else launch_hg4<4, 4, 1, 4, 16>(a, s, hg4_o64_w16_s4_kernel);
   }
 }
 
 // bf16 3x3 with 32-deep channel blocks.  Default: on a grid of >= 2 workgroups per CU, <= 256 channels in, <= 192
-// out, >= 93 % pixel-tile utilisation (tools/sweep_igemm.py, profiles/r2e_hg4_sweep.txt).  IC2_HG4=0 disables it, =2 forces it wherever legal (tests).
-static int hg4_mode() {
-  static const int mode = [] {
-    const char* e = getenv("IC2_HG4");
-    return e ? atoi(e) : 1;
-  }();
-  return mode;
-}
-static bool hg4_legal(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
-  if (!(dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 32 == 0 && cout_p % 64 == 0 &&
-        x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob))
-    return false;
-  return true;
+// out, >= 93 % pixel-tile utilisation (tools/sweep_igemm.py, profiles/r2e_hg4_sweep.txt).  Knob IC2_HG4 (IC2_DEV=1):
+// 0 disables it, 2 forces it wherever legal (the tests' forced-instance runs).
+static bool hg4_legal(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems) {
+  return dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 32 == 0 && cout_p % 64 == 0 &&
+         x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob;
 }
 static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
-  const int mode = hg4_mode();
-  if (!mode || !hg4_legal(dtype, cin_p, cout_p, kh, kw, x_elems, n, ho, wo)) return false;
+  static const int mode = knob("IC2_HG4", 1);
+  if (!mode || !hg4_legal(dtype, cin_p, cout_p, kh, kw, x_elems)) return false;
   if (mode == 2) return true;
   const H4Plan p = h4_plan(n, ho, wo, cout_p);
   if (p.blocks < 512) return false;
   const int th = (p.bo <= 128 ? 256 : 128) / (p.tw32 ? 32 : 16);
   const double util = (double)ho * wo / ((double)ceil_div(ho, th) * th * ceil_div(wo, p.tw32 ? 32 : 16) * (p.tw32 ? 32 : 16));
-  static const int max_cout = hg4_env("IC2_HG4_MAXC", 192);  // the 256-wide layers measured faster on hgemm
-  return cin_p <= 256 && cout_p <= max_cout && util >= 0.93;
-}
-
-static void hgemm_dispatch(const IgemmArgs& a, hipStream_t s) {
-  const HgPlan p = hg_plan(a.n, a.ho, a.wo, a.cout_p);
-  if (p.og2) {
-    if (p.tw32) launch_hgemm<2, 32>(a, s);
-    else launch_hgemm<2, 16>(a, s);
-  } else {
-    if (p.tw32) launch_hgemm<1, 32>(a, s);
-    else launch_hgemm<1, 16>(a, s);
-  }
+  return cin_p <= 256 && cout_p <= 192 && util >= 0.93;
 }
 
 // ------------------------------------------------------------------------------------------------
 // launch plan: tile instance and K split.  Tile ids: 0 = f32 128x128 (2-stage); bf16: 1 = 256x256,
 // 2 = 32x256, 3 = 128x256, 4 = 128x128, 5 = 64x256 (4-stage ring), 6 = 8-phase 256x256, 7 = 8-phase 128x512.
-// IC2_IGEMM_TILE=1..7 forces a bf16 tile (tests exercise every instance on small problems),
-// IC2_IGEMM_G8N=0 keeps the cout_p <= 128 layers off the 8-phase kernel, IC2_IGEMM_SPLITK=0 disables split-K.
+// Knobs (IC2_DEV=1 only): IC2_IGEMM_TILE=1..7 forces a bf16 tile (the tests exercise every instance on small
+// problems), IC2_IGEMM_G8N=0 keeps the cout_p <= 128 layers off the 8-phase kernel, IC2_IGEMM_SPLITK=0 disables
+// split-K.
 struct IgPlan {
   int tile, bo, bp, splits;
 };
 
-static bool ig_env_off(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '0';
-}
-
 static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int kw, int64_t x_elems) {
   static const int BOs[8] = {128, 256, 32, 128, 128, 64, 256, 128};
   static const int BPs[8] = {128, 256, 256, 256, 128, 256, 256, 512};
-  static const int forced = [] {
-    const char* e = getenv("IC2_IGEMM_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  static const bool g8n = !ig_env_off("IC2_IGEMM_G8N");
-  static const bool splitk = !ig_env_off("IC2_IGEMM_SPLITK");
+  static const int forced = knob("IC2_IGEMM_TILE", 0);
+  static const bool g8n = knob("IC2_IGEMM_G8N", 1) != 0;
+  static const bool splitk = knob("IC2_IGEMM_SPLITK", 1) != 0;
   const int64_t K = (int64_t)kh * kw * cin_p;
   int tile = 0;
   if (dtype == IC2_BF16) {
@@ -1578,9 +1276,9 @@ static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
 }
 
 // the halo kernel for bf16 3x3 convs with cin_p in {32, 64, 96}, cout_p in {32, 64} and >= 64K output
-// pixels; IC2_HCONV=0 keeps them on the implicit GEMM
+// pixels; knob IC2_HCONV=0 keeps them on the implicit GEMM
 static bool hconv_eligible(int dtype, int64_t M, int cin_p, int cout_p, int kh, int kw) {
-  static const bool on = !ig_env_off("IC2_HCONV");
+  static const bool on = knob("IC2_HCONV", 1) != 0;
   return on && dtype == IC2_BF16 && kh == 3 && kw == 3 && (cin_p == 32 || cin_p == 64 || cin_p == 96) &&
          (cout_p == 32 || cout_p == 64) && M >= 65536;
 }
@@ -1640,7 +1338,7 @@ __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
 // (the kernel maps output pixel p to input pixel p: 1x1, no padding)
 static bool torgb_eligible(int dtype, int cin_p, int cout_valid, int kh, int kw, int pad, int out_layout,
                            int out_dtype) {
-  static const bool on = !ig_env_off("IC2_TORGB");
+  static const bool on = knob("IC2_TORGB", 1) != 0;
   return on && dtype == IC2_BF16 && kh == 1 && kw == 1 && pad == 0 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
          out_dtype == IC2_F32 && (cin_p == 32 || cin_p == 64 || cin_p == 128);
 }
@@ -1654,21 +1352,93 @@ static void launch_torgb(const IgemmArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((torgb_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The launch plan of ic2_conv_igemm_ws, in one place: the dispatcher, the workspace query and the plan-name query
+// (tests / bench) all read it, so what is tested and timed is what runs.
+enum ConvKind { CK_TORGB, CK_HG4, CK_HCONV, CK_IGEMM };
+struct ConvChoice {
+  ConvKind kind;
+  IgPlan pl;
+  bool split384;  // tile 7 on an odd multiple of 128 above 128: two 8-phase launches (og2 + og1)
+};
+
+static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, int h, int w_, int cin_p, int cout_p,
+                              int cout_valid, int kh, int kw, int pad) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  const int64_t M = (int64_t)n * ho * wo;
+  const int64_t x_elems = (int64_t)n * h * w_ * cin_p;
+  ConvChoice c;
+  c.pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, x_elems);
+  c.split384 = false;
+  if (torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype)) {
+    c.kind = CK_TORGB;
+    c.pl.splits = 1;
+    return c;
+  }
+  // hg4 ahead of the halo direct conv for >= 96 input channels (SG3-T-1024 L11: 1532 -> 1363 us at batch 8); the
+  // 32 / 64-channel encoder layers stay on hconv (faster there).  Knob IC2_HG4_HCONV = 0 / 1: never / always.
+  static const int hg4_over_hconv = knob("IC2_HG4_HCONV", -1);
+  const bool hg4_ok = hg4_eligible(dtype, cin_p, cout_p, kh, kw, x_elems, n, ho, wo);
+  const bool hg4_pref = hg4_over_hconv == 1 || (hg4_over_hconv < 0 && cin_p >= 96);
+  if (hg4_ok && hg4_pref) c.kind = CK_HG4;
+  else if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) c.kind = CK_HCONV;
+  else if (hg4_ok) c.kind = CK_HG4;
+  else c.kind = CK_IGEMM;
+  if (c.kind != CK_IGEMM) {
+    c.pl.splits = 1;
+    return c;
+  }
+  // an odd multiple of 128 above 128 (384: SG3-T-256 L9, SG3-T-1024 L7): the 256-wide tile on all but the last
+  // 128 channels, the 128 x 512 tile on those (both read the same input panel); knob IC2_IGEMM_SPLIT=0 keeps one
+  // 128 x 512 launch
+  static const bool split = knob("IC2_IGEMM_SPLIT", 1) != 0;
+  c.split384 = dtype == IC2_BF16 && c.pl.tile == 7 && split && cout_p % 256 == 128 && cout_p > 128 &&
+               ceil_div(M, 256) >= 240;
+  return c;
+}
+
+static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int ho, int wo, int cin_p, int cout_p) {
+  static thread_local char buf[64];
+  switch (c.kind) {
+    case CK_TORGB: return "torgb";
+    case CK_HCONV:
+      snprintf(buf, sizeof(buf), "hconv_%d_%d", cin_p, cout_p);
+      return buf;
+    case CK_HG4: {
+      const H4Plan p = h4_plan(n, ho, wo, cout_p);
+      snprintf(buf, sizeof(buf), "hg4_o%d_w%s", p.bo, p.tw32 ? "32_hb" : "16_s4");
+      return buf;
+    }
+    default: break;
+  }
+  if (dtype != IC2_BF16) {
+    snprintf(buf, sizeof(buf), "igemm_f32_128x128%s", c.pl.splits > 1 ? "_splitk" : "");
+    return buf;
+  }
+  if (c.pl.tile == 6) return "igemm8_og2";
+  if (c.pl.tile == 7) return c.split384 ? "igemm8_og2+og1" : "igemm8_og1";
+  snprintf(buf, sizeof(buf), "igemm_%dx%d%s", c.pl.bo, c.pl.bp, c.pl.splits > 1 ? "_splitk" : "");
+  return buf;
+}
+
 }  // namespace ic2
 
 using namespace ic2;
+
+extern "C" const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, int n, int h, int w_, int cin_p,
+                                     int cout_p, int cout_valid, int kh, int kw, int pad) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (n <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0) return "invalid";
+  const ConvChoice c = conv_choice(dtype, out_layout, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  return conv_choice_name(c, dtype, n, ho, wo, cin_p, cout_p);
+}
 
 extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
                                            int pad) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
-  const int64_t M = (int64_t)n * ho * wo;
-  if ((hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo) ||
-       hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo)) &&
-      !hconv_eligible(dtype, M, cin_p, cout_p, kh, kw))
-    return 0;
-  const IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
-  return pl.splits > 1 ? (int64_t)pl.splits * M * cout_p * 4 : 0;
+  const ConvChoice c = conv_choice(dtype, IC2_LAYOUT_NHWC, dtype, n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad);
+  return c.kind == CK_IGEMM && c.pl.splits > 1 ? (int64_t)c.pl.splits * n * ho * wo * cout_p * 4 : 0;
 }
 
 extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
@@ -1702,74 +1472,56 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
   a.in_gn = nullptr; a.in_slope = 0.f;
   static const int group = [] {
-    const char* e = getenv("IC2_IGEMM_GROUP");
-    const int g = e ? atoi(e) : 1;  // 1 = o-tiles of a p-tile side by side (measured best)
+    const int g = knob("IC2_IGEMM_GROUP", 1);  // 1 = o-tiles of a p-tile side by side (measured best)
     return g >= 1 ? g : 1;
   }();
   a.group = group;
-  static const int korder = [] {
-    const char* e = getenv("IC2_IGEMM_KORDER");
-    return e ? atoi(e) : 1;  // channel-major: s148 +3 %, s148b +5 %, s148c +7 %, C2 +2.6 % (profiles/r2f_korder.txt)
-  }();
+  // channel-major K order: s148 +3 %, s148b +5 %, s148c +7 %, C2 +2.6 % (profiles/r2f_korder.txt)
+  static const int korder = knob("IC2_IGEMM_KORDER", 1);
   a.korder = korder;
   a.o_base = 0;
   hipStream_t s = as_stream(stream);
-  IgPlan pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, (int64_t)n * h * w_ * cin_p);
+  ConvChoice c = conv_choice(dtype, out_layout, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  IgPlan& pl = c.pl;
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
-  const bool torgb = torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype);
-  // hg4 ahead of the halo direct conv: for 96 input channels (SG3-T-1024 L11: 1532 -> 1363 us at batch 8); the
-  // 32 / 64-channel encoder layers stay on hconv (faster there).  IC2_HG4_HCONV=0 / 1: never / always.
-  static const int hg4_over_hconv = hg4_env("IC2_HG4_HCONV", -1);
-  const bool hg4_pref = hg4_over_hconv == 1 || (hg4_over_hconv < 0 && cin_p >= 96);
-  const bool hg4_first = hg4_pref && !torgb && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo);
-  const bool hconv = !torgb && !hg4_first && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
-  const bool hg4 = hg4_first ||
-                   (!torgb && !hconv && hg4_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo));
-  const bool hgemm =
-      !torgb && !hconv && (hg4 || hgemm_eligible(dtype, cin_p, cout_p, kh, kw, (int64_t)n * h * w_ * cin_p, n, ho, wo));
-  if (hgemm) pl.splits = 1;
-  if (torgb) {
-    launch_torgb(a, s);
-  } else if (hg4) {
-    hg4_dispatch(a, s);
-  } else if (hgemm) {
-    hgemm_dispatch(a, s);
-  } else if (hconv) {
-    if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
-    else if (cin_p == 32) launch_hconv<32, 64>(a, s);
-    else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
-    else if (cin_p == 64) launch_hconv<64, 64>(a, s);
-    else if (cout_p == 32) launch_hconv<96, 32>(a, s);
-    else launch_hconv<96, 64>(a, s);
-  } else if (dtype == IC2_BF16) {
-    switch (pl.tile) {
-      case 6: launch_g8<2>(a, s); break;
-      case 7: {
-        // an odd multiple of 128 above 128 (384: SG3-T-256 L9, SG3-T-1024 L7): the 256-wide tile on all but the
-        // last 128 channels, the 128 x 512 tile on those (both read the same input panel); IC2_IGEMM_SPLIT=0 keeps
-        // one 128 x 512 launch
-        static const bool split = !ig_env_off("IC2_IGEMM_SPLIT");
-        if (split && cout_p % 256 == 128 && cout_p > 128 && ceil_div(M, 256) >= 240) {
-          launch_g8<2>(a, s, 0, cout_p - 128);
-          launch_g8<1>(a, s, cout_p - 128, cout_p);
-        } else {
-          launch_g8<1>(a, s);
-        }
+  switch (c.kind) {
+    case CK_TORGB: launch_torgb(a, s); break;
+    case CK_HG4: hg4_dispatch(a, s); break;
+    case CK_HCONV:
+      if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
+      else if (cin_p == 32) launch_hconv<32, 64>(a, s);
+      else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
+      else if (cin_p == 64) launch_hconv<64, 64>(a, s);
+      else if (cout_p == 32) launch_hconv<96, 32>(a, s);
+      else launch_hconv<96, 64>(a, s);
+      break;
+    case CK_IGEMM:
+      if (dtype != IC2_BF16) {
+        launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
         break;
       }
-      case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, pl.splits, s); break;
-      case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, pl.splits, s); break;
-      case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, pl.splits, s); break;
-      case 5: launch_igemm<true, 64, 256, 1, 4, 4>(a, pl.splits, s); break;
-      default: launch_igemm<true, 128, 128, 2, 2, 4>(a, pl.splits, s); break;
-    }
-  } else {
-    launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
-  }
-  if (pl.splits > 1 && !torgb && !hconv && !hgemm) {
-    const int64_t total = M * (cout_p / 4);
-    const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
-    hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);
+      switch (pl.tile) {
+        case 6: launch_g8<2>(a, s); break;
+        case 7:
+          if (c.split384) {
+            launch_g8<2>(a, s, 0, cout_p - 128);
+            launch_g8<1>(a, s, cout_p - 128, cout_p);
+          } else {
+            launch_g8<1>(a, s);
+          }
+          break;
+        case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, pl.splits, s); break;
+        case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, pl.splits, s); break;
+        case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, pl.splits, s); break;
+        case 5: launch_igemm<true, 64, 256, 1, 4, 4>(a, pl.splits, s); break;
+        default: launch_igemm<true, 128, 128, 2, 2, 4>(a, pl.splits, s); break;
+      }
+      if (pl.splits > 1) {
+        const int64_t total = M * (cout_p / 4);
+        const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
+        hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);
+      }
+      break;
   }
   IC2_CHECK_LAUNCH("conv_igemm");
   return IC2_OK;
@@ -1798,11 +1550,8 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   // fused instances: 32 groups over all cout_p channels (VGGBlock: GroupNorm(min(32, c), c) with c = 32 / 64).
   // Off by default: measured on MI355X the epilogue reduction (two extra barriers per tile in the persistent
   // kernel) costs what the saved read of y gains -- C4 357.1 -> 356.7 img/s, C2 1277 -> 1256 (profiles/
-  // r2b_conv_gn_ab.txt); IC2_CONV_GN=1 enables it.
-  static const bool fuse_env = [] {
-    const char* e = getenv("IC2_CONV_GN");
-    return e && e[0] == '1';
-  }();
+  // r2b_conv_gn_ab.txt); knob IC2_CONV_GN=1 enables it.
+  static const bool fuse_env = knob("IC2_CONV_GN", 0) == 1;
   const bool fuse_req = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
   const bool fuse = fuse_req && hconv && part != nullptr && part_doubles >= (int64_t)n * groups * nch * 2 &&
                     groups == 32 && cout_valid == cout_p && bias != nullptr;

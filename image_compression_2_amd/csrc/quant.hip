@@ -316,3 +316,58 @@ extern "C" int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const floa
   IC2_CHECK_LAUNCH("gumbel_softmax_quantize");
   return IC2_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Per-batch code record for the metric all_reduce ([.., n_index_mismatch, hist[256]]; the
+// reference's usage / perplexity are over the whole batch, gumbel_softmax_compression.py:121-127).
+// kind 0: f32 uniform-quantized latents q (ic2_quantize_uniform's output) -> code round((q + 1) * 0.5 * S), exact for
+// q on the grid; kind 1: int64 codebook indices.  counts [k + 2] uint32 (zeroed by the caller) accumulate
+// hist[0 .. k), the codes outside [0, k) in counts[k], and the elements differing from `golden` (nullable, same
+// kind) in counts[k + 1].  LDS histogram per workgroup, one global (vector) atomic add per bin.
+namespace ic2 {
+template <int KIND>
+__global__ void __launch_bounds__(256) code_record_kernel(const void* __restrict__ codes, const void* __restrict__ golden,
+                                                          int64_t n, int k, float S, uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t sh[];
+  for (int i = threadIdx.x; i < k + 2; i += 256) sh[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    int64_t c;
+    bool diff = false;
+    if constexpr (KIND == 0) {
+      const float q = reinterpret_cast<const float*>(codes)[i];
+      c = (int64_t)rintf(((q + 1.0f) * 0.5f) * S);
+      if (golden) diff = __float_as_uint(q) != __float_as_uint(reinterpret_cast<const float*>(golden)[i]);
+    } else {
+      c = reinterpret_cast<const int64_t*>(codes)[i];
+      if (golden) diff = c != reinterpret_cast<const int64_t*>(golden)[i];
+    }
+    atomicAdd(&sh[(c >= 0 && c < k) ? (int)c : k], 1u);
+    if (diff) atomicAdd(&sh[k + 1], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k + 2; i += 256)
+    if (sh[i]) atomicAdd(&counts[i], sh[i]);
+}
+}  // namespace ic2
+
+extern "C" int ic2_code_record(const void* codes, int kind, int k, int bits, const void* golden, int64_t n,
+                               uint32_t* counts, void* stream) {
+  IC2_CHECK_ARG(codes && counts && n >= 0 && k > 0 && k <= 8192 && (kind == 0 || kind == 1),
+                "code_record: bad arguments");
+  IC2_CHECK_ARG(kind == 1 || (bits >= 1 && bits <= 16 && k == (1 << bits)), "code_record: uniform codes need k = 2^bits");
+  if (n == 0) return IC2_OK;
+  const int64_t g = ceil_div(n, 256 * 8);
+  const unsigned grid = (unsigned)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  const size_t lds = (size_t)(k + 2) * sizeof(uint32_t);
+  const float S = (float)((1 << (kind == 0 ? bits : 1)) - 1);
+  if (kind == 0)
+    hipLaunchKernelGGL(code_record_kernel<0>, dim3(grid), dim3(256), lds, as_stream(stream), codes, golden, n, k, S,
+                       counts);
+  else
+    hipLaunchKernelGGL(code_record_kernel<1>, dim3(grid), dim3(256), lds, as_stream(stream), codes, golden, n, k, S,
+                       counts);
+  IC2_CHECK_LAUNCH("code_record");
+  return IC2_OK;
+}

@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, in
 // ------------------------------------------------------------------------------------------------
 // weight packing [cout][cin][kh][kw] f32 -> [cout_p][kh][kw][cin_p] (dtype); optional pre-normalisation
 // ------------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, bool X3 = false>
 __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int kh,
                                                           int kw, int cout_p, int cin_p, int prenorm, float gscale,
                                                           T* __restrict__ out, float* __restrict__ wsq) {
@@ -171,7 +171,17 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
     const int k = e / cin_p;
     float v = 0.f;
     if (o < cout && i < cin) v = w[((int64_t)o * cin + i) * kk + k] * scale * gscale;
-    st(out + (int64_t)o * total + e, v);
+    if constexpr (X3) {
+      // split bf16: [hi | lo | hi] along the tripled channel axis of tap k (ic2ops.h IC2_BF16X3)
+      bf16_t* row = reinterpret_cast<bf16_t*>(out) + ((int64_t)o * kk + k) * 3 * cin_p + i;
+      const bf16_t hi = f2bf(v);
+      const bf16_t lo = f2bf(v - bf2f(hi));
+      row[0] = hi;
+      row[cin_p] = lo;
+      row[2 * cin_p] = hi;
+    } else {
+      st(out + (int64_t)o * total + e, v);
+    }
   }
   if (wsq && o < cout) {
     for (int i = threadIdx.x; i < cin; i += 256) {
@@ -496,6 +506,9 @@ extern "C" int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p, cin_p,
                        prenorm, scale, (bf16_t*)w_out, wsq_out);
+  else if (dtype == IC2_BF16X3)
+    hipLaunchKernelGGL((pack_weight_kernel<bf16_t, true>), dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p,
+                       cin_p, prenorm, scale, (bf16_t*)w_out, wsq_out);
   else
     IC2_CHECK_ARG(false, "pack_weight: bad dtype %d", dtype);
   IC2_CHECK_LAUNCH("pack_weight");

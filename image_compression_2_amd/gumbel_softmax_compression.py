@@ -7,7 +7,8 @@ Indices are bit-exact (fp32 |z - c| argmin, first index on ties, ref :97, :118).
 comes from an in-kernel Philox stream seeded from torch's CPU generator: the same distribution as
 ``F.gumbel_softmax``, not the same stream (the reference's noisy outputs are RNG-dependent anyway,
 SURVEY.md 0 quirk 3); compress()/decompress() are deterministic and bit-exact.
-Forward is inference-only (no autograd through the kernel; training is out of scope).
+Forward is inference-only: it runs in grad mode, but a backward through the kernel raises (training is out of
+scope).
 """
 from __future__ import annotations
 
@@ -79,7 +80,7 @@ class GumbelSoftmaxDiscretization(nn.Module):
         batch_size, num_ws, w_dim = z.shape
         if hard is None:
             hard = not self.training
-        nv.forbid_autograd("GumbelSoftmaxDiscretization.forward", (z, self.log_temperature))
+        z_in = z
         z = z.to(torch.float32).contiguous()
         nv.require_gpu(z)
         m = z.numel()
@@ -101,7 +102,9 @@ class GumbelSoftmaxDiscretization(nn.Module):
             self.usage += hist.to(self.usage.dtype)
         avg_probs = psum / m
         perplexity = torch.exp(-torch.sum(avg_probs * torch.log(avg_probs + 1e-10)))
-        return disc.view(batch_size, num_ws, w_dim), perplexity, idx
+        # inference in grad mode works; a backward through the fused kernel raises (training is out of scope)
+        return nv.refuse_backward("GumbelSoftmaxDiscretization.forward", (disc.view(batch_size, num_ws, w_dim),
+                                  perplexity, idx), (z_in, self.log_temperature))
 
     def get_code_usage(self):
         total = self.usage.sum().float()
@@ -142,11 +145,16 @@ class GumbelSoftmaxCompressor(nn.Module):
 
     def compress(self, x, discrete_bits=8):
         """-> int64 codes [B, num_ws, w_dim] on the CPU (ref :213-235); exact argmin kernel."""
+        return self.compress_codes(x, discrete_bits).cpu()
+
+    def compress_codes(self, x, discrete_bits=8):
+        """compress() with the codes left on the device (extension): the reference's indices (argmin |means - c|,
+        first index on ties, gumbel_softmax_compression.py:229) without its device -> host copy (:235)."""
         with torch.no_grad():
             w_plus, means, _ = self.encoder(x)
             indices = codebook_argmin(means, self.discretization.codebook)
             batch_size, num_ws, w_dim = w_plus.shape
-            return indices.reshape(batch_size, num_ws, w_dim).cpu()
+            return indices.reshape(batch_size, num_ws, w_dim)
 
     def decompress(self, codes, noise_mode="const"):
         with torch.no_grad():

@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import scipy.signal
@@ -35,25 +34,25 @@ from . import _native as nv
 from . import autograd_ops as ao
 from . import sg3_ops
 
-# conv -> filtered lrelu hand-off in the channel-blocked NHWC16 layout (bf16 mode); IC2_FLR_BLOCKED=0: plain NHWC
-_FLR_BLOCKED = os.environ.get("IC2_FLR_BLOCKED", "1") != "0"
+# conv -> filtered lrelu hand-off in the channel-blocked NHWC16 layout (bf16 mode); knob IC2_FLR_BLOCKED=0 (IC2_DEV=1):
+# plain NHWC
+_FLR_BLOCKED = nv.knob("IC2_FLR_BLOCKED", 1) != 0
 
 
 def _train_mode(module, *tensors):
-    """Autograd path wanted: grad mode on and an input requires grad.  Generator weights are frozen on that
-    path (the reference freezes G, stylegan3_hvae_full.py:259-261); weight gradients are refused."""
+    """Autograd path wanted: grad mode on, an input requires grad and the module's weights are frozen (the
+    reference trains its encoder through a frozen G, stylegan3_hvae_full.py:259-261).  With unfrozen weights the
+    inference path runs and its output refuses backward (_refuse): gradients w.r.t. the generator's weights are
+    not implemented."""
     if not torch.is_grad_enabled():
         return False
-    params = any(p.requires_grad for p in module.parameters())
-    if not any(t is not None and t.requires_grad for t in tensors):
-        if params:
-            nv.forbid_autograd(type(module).__name__ + ".forward", (), (module,))
+    if any(p.requires_grad for p in module.parameters()):
         return False
-    if params:
-        raise nv.AutogradUnsupported(
-            f"{type(module).__name__}.forward: gradients w.r.t. the generator's weights are not implemented "
-            "(the reference trains its encoder through a frozen G): call .requires_grad_(False) on the generator")
-    return True
+    return any(t is not None and t.requires_grad for t in tensors)
+
+
+def _refuse(module, out, *tensors):
+    return nv.refuse_backward(type(module).__name__ + ".forward", out, tensors, (module,))
 
 
 def _version_key(*tensors):
@@ -89,12 +88,12 @@ class FullyConnectedLayer(torch.nn.Module):
         return out
 
     def forward(self, x):
-        nv.forbid_autograd("FullyConnectedLayer.forward", (x,), (self,))
+        xin = x
         x = x.to(torch.float32).contiguous()
         nv.require_gpu(x)
         if self.activation not in ("linear", "lrelu"):
             raise NotImplementedError(self.activation)
-        return self.run(x)
+        return _refuse(self, self.run(x), xin)
 
     def extra_repr(self):
         return f"in_features={self.in_features:d}, out_features={self.out_features:d}, activation={self.activation:s}"
@@ -119,7 +118,6 @@ class MappingNetwork(torch.nn.Module):
     def forward(self, z, c=None, truncation_psi=1, truncation_cutoff=None, update_emas=False):
         if update_emas:
             raise NotImplementedError("update_emas is a training feature (out of scope)")
-        nv.forbid_autograd("MappingNetwork.forward", (z,), (self,))
         x = z.to(torch.float32).contiguous()
         nv.require_gpu(x)
         x = x * (x.square().mean(1, keepdim=True) + 1e-8).rsqrt()
@@ -129,7 +127,7 @@ class MappingNetwork(torch.nn.Module):
         if truncation_psi != 1:
             cut = self.num_ws if truncation_cutoff is None else truncation_cutoff
             x[:, :cut] = self.w_avg.lerp(x[:, :cut], truncation_psi)
-        return x
+        return _refuse(self, x, z)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -179,6 +177,7 @@ class SynthesisInput(torch.nn.Module):
                 nv.stream_of(ws))
         out = torch.empty([n, S, S, cp], dtype=dt, device=dev)
         w = self.packed_weight(dt)
+        nv.note_flops(2 * n * S * S * C * C)
         nv.conv_igemm(nv.ptr(feats), nv.ptr(w), nv.ptr(out), nv.dtype_code(dt), nv.dtype_code(dt), n, S, S, cp, cp, C,
                       1, 1, 0, S, S, nv.ptr(post_scale), None, 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(ws),
                       feats.device)
@@ -212,13 +211,14 @@ class SynthesisInput(torch.nn.Module):
     def forward(self, w):
         if _train_mode(self, w):
             return self.forward_train_nhwc(w.to(torch.float32)).permute(0, 3, 1, 2).contiguous()
+        w_in = w
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(w)
         n, S, C, cp = w.shape[0], int(self.size[0]), self.channels, nv.pad_synth(self.channels)
         x = self.run_nhwc(w, self.w_dim, n, torch.float32, None)
         y = torch.empty([n, C, S, S], dtype=torch.float32, device=w.device)
         nv.call("ic2_nhwc_to_nchw", nv.ptr(x), nv.F32, nv.ptr(y), n, C, S, S, cp, nv.stream_of(w))
-        return y
+        return _refuse(self, y, w_in)
 
     def extra_repr(self):
         return (f"w_dim={self.w_dim:d}, channels={self.channels:d}, size={list(self.size)}, "
@@ -354,6 +354,7 @@ class SynthesisLayer(torch.nn.Module):
         conv = s_in + 2 * pad - k + 1
         wp, _, bp = self.packed(dt)
         stream = nv.stream_of(x)
+        nv.note_flops(2 * n * conv * conv * self.out_channels * self.in_channels * k * k)
         if self.is_torgb:
             assert self.up_factor == 1 and self.down_factor == 1 and self.padding == [0, 0, 0, 0]
             out = torch.empty([n, self.out_channels, conv, conv], dtype=torch.float32, device=x.device)
@@ -451,6 +452,7 @@ class SynthesisLayer(torch.nn.Module):
             raise NotImplementedError("update_emas is a training feature (out of scope)")
         if _train_mode(self, x, w):
             return self.forward_train(x, w)
+        x_in, w_in = x, w
         x = x.to(torch.float32).contiguous()
         w = w.to(torch.float32).contiguous()
         nv.require_gpu(x, w)
@@ -464,12 +466,12 @@ class SynthesisLayer(torch.nn.Module):
                 nv.ptr(xs), nv.stream_of(x))
         out = self.run_nhwc(xn, n, dt, os_, None)
         if self.is_torgb:
-            return out
+            return _refuse(self, out, x_in, w_in)
         s_out = int(self.out_size[0])
         y = torch.empty([n, self.out_channels, s_out, s_out], dtype=torch.float32, device=x.device)
         nv.call("ic2_nhwc_to_nchw", nv.ptr(out), nv.F32, nv.ptr(y), n, self.out_channels, s_out, s_out, self.cout_p,
                 nv.stream_of(x))
-        return y
+        return _refuse(self, y, x_in, w_in)
 
     def forward_train(self, x, w):
         """Layer-level autograd path (NCHW f32 in/out), fp32."""
@@ -565,6 +567,7 @@ class SynthesisNetwork(torch.nn.Module):
         dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
         if _train_mode(self, ws):
             return self.forward_train(ws, dt)
+        ws_in = ws
         ws = ws.to(torch.float32).contiguous()
         nv.require_gpu(ws)
         n = ws.shape[0]
@@ -577,7 +580,7 @@ class SynthesisNetwork(torch.nn.Module):
         for i, L in enumerate(layers):
             post = sc[i + 1][0] if i + 1 < len(layers) else None
             x = L.run_nhwc(x, n, dt, sc[i][1], post, final_scale=self.output_scale if L.is_torgb else None)
-        return x
+        return _refuse(self, x, ws_in)
 
     def scales_batched(self, ws, ldx, n, dt):
         """[(xscale [n][cin_p], oscale [n][cout_p]) per layer] through ic2_modconv_prep_batched."""

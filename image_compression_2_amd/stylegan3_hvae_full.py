@@ -17,7 +17,6 @@ opt-in extension.
 """
 from __future__ import annotations
 
-import os
 import types
 
 import numpy as np
@@ -35,33 +34,51 @@ def _version_key(*tensors):
 
 
 class _Act:
-    """NHWC activation handle: tensor [n, h, w, c_p] + logical channel count."""
-    __slots__ = ("t", "n", "h", "w", "c", "c_p")
+    """NHWC activation handle: tensor [n, h, w, c_p] + logical channel count.  x3: split bf16 (ic2ops.h
+    IC2_BF16X3), the tensor holds 3 * c_p bf16 channels [hi | hi | lo] per pixel."""
+    __slots__ = ("t", "n", "h", "w", "c", "c_p", "x3")
 
-    def __init__(self, t, c):
+    def __init__(self, t, c, x3=False):
         self.t = t
-        self.n, self.h, self.w, self.c_p = t.shape
+        self.n, self.h, self.w, cp = t.shape
+        self.c_p = cp // 3 if x3 else cp
         self.c = c
+        self.x3 = x3
+
+    @property
+    def k_p(self):
+        """Channel stride the conv's GEMM sees (the tripled one in split mode)."""
+        return 3 * self.c_p if self.x3 else self.c_p
+
+    @property
+    def code(self):
+        return nv.BF16X3 if self.x3 else nv.dtype_code(self.t.dtype)
 
 
 def _packed(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     cout, cin, kh, kw = conv.weight.shape
     assert conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and cin == x.c
-    pad = conv.padding[0]
-    key = (dt, _version_key(conv.weight, conv.bias))
+    x3 = bool(getattr(x, "x3", False))
+    key = (dt, x3, _version_key(conv.weight, conv.bias))
     hit = cache.get(id(conv))
     if hit is None or hit[0] != key:
         w = conv.weight.detach().to(torch.float32).contiguous()
         cout_p, cin_p = nv.pad32(cout), x.c_p
-        wp = torch.empty([cout_p, kh, kw, cin_p], dtype=dt, device=w.device)
-        nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(wp), nv.dtype_code(dt),
-                None, stream)
+        # split mode: [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi] against the activation's [hi | hi | lo]
+        wp = torch.empty([cout_p, kh, kw, 3 * cin_p if x3 else cin_p], dtype=dt, device=w.device)
+        nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(wp),
+                nv.BF16X3 if x3 else nv.dtype_code(dt), None, stream)
         bp = torch.zeros([cout_p], dtype=torch.float32, device=w.device)
         if conv.bias is not None:
             bp[:cout] = conv.bias.detach().float()
         hit = (key, (wp, bp))
         cache[id(conv)] = hit
     return hit[1]
+
+
+def _conv_flops(n, ho, wo, cout, cin, kh, kw):
+    """Algorithmic FLOPs of an nn.Conv2d launch (unpadded channels): what the reference computes."""
+    return 2 * n * ho * wo * cout * cin * kh * kw
 
 
 def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
@@ -72,30 +89,56 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
     y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
+    nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
     nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.t.dtype), nv.dtype_code(dt), x.n, x.h, x.w,
                   x.c_p, cout_p, cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream,
                   x.t.device)
     return _Act(y, cout)
 
 
-# IC2_FROM_RGB_DIRECT=0 keeps the packing + implicit-GEMM from_rgb (A/B switch)
-_FROM_RGB_DIRECT = os.environ.get("IC2_FROM_RGB_DIRECT", "1") != "0"
-# IC2_GN_IN_FUSE=1 applies norm1 + lrelu inside conv2's halo-conv staging instead of materialising it.  Bit-identical
+# knob IC2_FROM_RGB_DIRECT=0 (IC2_DEV=1) keeps the packing + implicit-GEMM from_rgb (A/B switch)
+_FROM_RGB_DIRECT = nv.knob("IC2_FROM_RGB_DIRECT", 1) != 0
+# knob IC2_GN_IN_FUSE=1 applies norm1 + lrelu inside conv2's halo-conv staging instead of materialising it.  Bit-identical
 # but measured level on MI355X (C2 1438.0 -> 1439.4, C4 415.5 -> 415.9 img/s, same box: the saved pass is paid back in
 # the heavier staging of the 64-channel halo conv), so off by default
-_GN_IN_FUSE = os.environ.get("IC2_GN_IN_FUSE", "0") == "1"
+_GN_IN_FUSE = nv.knob("IC2_GN_IN_FUSE", 0) == 1
 
 
-def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream):
+def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream, split=False):
     """from_rgb on the NCHW f32 image: in bf16 mode one direct kernel (ic2_from_rgb_conv: no 32-channel packed copy
-    of the image), else the packing + implicit GEMM."""
+    of the image), else the packing + implicit GEMM.  split: the encoder's bf16x3 mode -- exact f32 arithmetic, the
+    output stored split for the next conv (ic2_from_rgb_conv_x3, or an f32 conv + split packing)."""
     cout, cin, kh, kw = conv.weight.shape
+    if split:
+        n, _, hh, ww = x.shape
+        cout_p = nv.pad32(cout)
+        bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
+        bp[:cout] = conv.bias.detach().float()
+        y = torch.empty([n, hh, ww, 3 * cout_p], dtype=torch.bfloat16, device=x.device)
+        if cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1 and cout_p in (32, 64, 128):
+            wf = conv.weight.detach().to(torch.float32).contiguous()
+            nv.note_flops(_conv_flops(n, hh, ww, cout, cin, 3, 3))
+            nv.call("ic2_from_rgb_conv_x3", nv.ptr(x), cin, nv.ptr(wf), cout, nv.ptr(bp), nv.ptr(y), n, hh, ww, cout_p,
+                    stream)
+        else:
+            xf = _to_nhwc(x, torch.float32, stream)
+            wp, bq = _packed(conv, xf, torch.float32, cache, stream)
+            pad = conv.padding[0]
+            ho, wo = hh + 2 * pad - kh + 1, ww + 2 * pad - kw + 1
+            yf = torch.empty([n, cout, ho, wo], dtype=torch.float32, device=x.device)
+            nv.note_flops(_conv_flops(n, ho, wo, cout, cin, kh, kw))
+            nv.conv_igemm(nv.ptr(xf.t), nv.ptr(wp), nv.ptr(yf), nv.F32, nv.F32, n, hh, ww, xf.c_p, cout_p, cout, kh, kw,
+                          pad, ho, wo, None, nv.ptr(bq), 0, 0.0, 1.0, -1.0, 1.0, nv.NCHW, stream, x.device)
+            y = torch.empty([n, ho, wo, 3 * cout_p], dtype=torch.bfloat16, device=x.device)
+            nv.call("ic2_nchw_to_nhwc", nv.ptr(yf), nv.ptr(y), nv.BF16X3, n, cout, ho, wo, cout_p, None, stream)
+        return _Act(y, cout, x3=True)
     if (dt == torch.bfloat16 and cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1
             and nv.pad32(cout) in (32, 64) and _FROM_RGB_DIRECT):
         n, _, hh, ww = x.shape
         fake = types.SimpleNamespace(c=cin, c_p=nv.pad32(cin))
         wp, bp = _packed(conv, fake, dt, cache, stream)
         y = torch.empty([n, hh, ww, wp.shape[0]], dtype=dt, device=x.device)
+        nv.note_flops(_conv_flops(n, hh, ww, cout, cin, kh, kw))
         nv.call("ic2_from_rgb_conv", nv.ptr(x), cin, nv.ptr(wp), fake.c_p, nv.ptr(bp), nv.ptr(y), n, hh, ww,
                 wp.shape[0], stream)
         return _Act(y, cout)
@@ -111,12 +154,25 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     wp, bp = _packed(conv, x, dt, cache, stream)
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
+    if x.x3:
+        # split bf16: one bf16 implicit GEMM over the tripled K, f32 out, GroupNorm statistics on the f32 values
+        y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
+        nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
+        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
+                      pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.t.device)
+        ya = _Act(y, cout)
+        nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
+        stats = torch.empty([nfl], dtype=torch.float32, device=y.device)
+        nv.call("ic2_group_norm_stats", nv.ptr(y), nv.F32, ya.n, ya.h * ya.w, ya.c_p, ya.c, norm.num_groups,
+                float(norm.eps), nv.ptr(stats), stream)
+        return ya, stats
     dc = nv.dtype_code(dt)
     y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
     nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad, norm.num_groups))
     stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
     nbytes = int(nv.query("ic2_conv_igemm_ws_bytes", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad))
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=x.t.device) if nbytes > 0 else None
+    nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
     if in_gn is not None:
         nv.call("ic2_conv3x3_gnin_gn_fwd", nv.ptr(x.t), nv.ptr(in_gn[0]), float(in_gn[1]), nv.ptr(wp), nv.ptr(y), dc,
                 x.n, x.h, x.w, x.c_p, cout_p, cout, kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps),
@@ -143,8 +199,9 @@ def _gn_affine_table(norm: nn.GroupNorm, y: _Act, stats, stream):
     return table
 
 
-def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None):
-    """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2)); `stats` from _conv_gn, else computed here."""
+def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None, split=False):
+    """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2)); `stats` from _conv_gn, else computed here.
+    split: f32 arithmetic, output stored split bf16 (the next conv's operand in bf16x3 mode)."""
     groups = norm.num_groups
     if stats is None:
         nfl = int(nv.query("ic2_group_norm_stats_floats", y.n, y.h * y.w, groups))
@@ -152,17 +209,17 @@ def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope
         nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
                 float(norm.eps), nv.ptr(stats), stream)
     oh, ow = (y.h // 2, y.w // 2) if pool else (y.h, y.w)
-    out = torch.empty([y.n, oh, ow, y.c_p], dtype=dt, device=y.t.device)
-    nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype), nv.dtype_code(dt), y.n, y.h, y.w,
-            y.c_p, y.c, groups, nv.ptr(stats), nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)
-    return _Act(out, y.c)
+    out = torch.empty([y.n, oh, ow, 3 * y.c_p if split else y.c_p], dtype=dt, device=y.t.device)
+    nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype),
+            nv.BF16X3 if split else nv.dtype_code(dt), y.n, y.h, y.w, y.c_p, y.c, groups, nv.ptr(stats),
+            nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)
+    return _Act(out, y.c, x3=split)
 
 
 def _gap(x: _Act, stream):
     nfl = int(nv.query("ic2_global_avg_pool_floats", x.n, x.h * x.w, x.c_p, x.c))
     buf = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
-    nv.call("ic2_global_avg_pool", nv.ptr(x.t), nv.dtype_code(x.t.dtype), x.n, x.h * x.w, x.c_p, x.c, nv.ptr(buf),
-            stream)
+    nv.call("ic2_global_avg_pool", nv.ptr(x.t), x.code, x.n, x.h * x.w, x.c_p, x.c, nv.ptr(buf), stream)
     return buf[: x.n * x.c].view(x.n, x.c)
 
 
@@ -200,6 +257,9 @@ class HVAE_VGG_Encoder(nn.Module):
 
     def __init__(self, img_resolution=1024, img_channels=3, w_dim=512, num_ws=16, block_split=(5, 12),
                  channel_base=32768, channel_max=512, use_fp16=False, precision="fp32"):
+        """precision (extension, not in the reference): 'fp32' (parity, exact-f32 MFMA), 'bf16' (bf16 storage and
+        MFMA), 'bf16x3' (split bf16: three bf16 MFMA terms per product, f32 storage -- latents at fp32 level, the
+        8-bit indices of the fp32 reference)."""
         super().__init__()
         self.img_resolution = img_resolution
         self.img_channels = img_channels
@@ -208,7 +268,7 @@ class HVAE_VGG_Encoder(nn.Module):
         self.block_split = block_split
         self.use_fp16 = use_fp16
         self.precision = precision
-        nv.torch_dtype(precision)
+        nv.encoder_dtype(precision)
         self.num_layers = int(np.log2(img_resolution))
         channels = {}
         for res in range(self.num_layers + 1):
@@ -229,13 +289,13 @@ class HVAE_VGG_Encoder(nn.Module):
         self._cache = {}
 
     def set_precision(self, precision):
-        nv.torch_dtype(precision)
+        nv.encoder_dtype(precision)
         self.precision = precision
         return self
 
-    def features_nhwc(self, x, dt, stream):
+    def features_nhwc(self, x, dt, stream, split=False):
         """from_rgb + blocks with the reference's 1x1 break; returns {'fine','medium','global'} -> _Act."""
-        h = _from_rgb(self.from_rgb, x, dt, self._cache, stream)
+        h = _from_rgb(self.from_rgb, x, dt, self._cache, stream, split=split)
         feats = {}
         for i, block in enumerate(self.blocks):
             if h.h <= 1 or h.w <= 1:
@@ -257,9 +317,9 @@ class HVAE_VGG_Encoder(nn.Module):
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             return self.forward_train(x)
         x = _check_input(x)
-        dt = nv.torch_dtype(self.precision)
+        dt, split = nv.encoder_dtype(self.precision)
         stream = nv.stream_of(x)
-        feats = self.features_nhwc(x, dt, stream)
+        feats = self.features_nhwc(x, dt, stream, split=split)
         n = x.shape[0]
         outs = [torch.empty([n, self.num_ws, self.w_dim], dtype=torch.float32, device=x.device) for _ in range(3)]
         off = 0
@@ -271,10 +331,11 @@ class HVAE_VGG_Encoder(nn.Module):
 
 
     def forward_train(self, x):
-        """Autograd path: NHWC activations in the module's precision, HIP forward + backward kernels per op."""
+        """Autograd path: NHWC activations in the module's precision, HIP forward + backward kernels per op
+        ('bf16x3', an inference precision, trains in bf16)."""
         x = x.to(torch.float32)
         nv.require_gpu(x.contiguous())
-        dt = nv.torch_dtype(self.precision)
+        dt, _ = nv.encoder_dtype(self.precision)
         h = ao.ToNHWC.apply(x.contiguous(), dt, nv.pad32(x.shape[1]))
         h = ao.Conv2dNHWC.apply(h, self.from_rgb.weight, self.from_rgb.bias, self.from_rgb.padding[0],
                                 nv.pad32(self.from_rgb.out_channels))
@@ -312,16 +373,17 @@ class VGGBlock(nn.Module):
         self._cache = {}
 
     def run_nhwc(self, x: _Act, dt, cache, stream):
+        split = x.x3
         y, st = _conv_gn(self.conv1, self.norm1, x, dt, cache, stream)
-        if _gn_in_fusable(self.conv2, y, dt):
+        if not split and _gn_in_fusable(self.conv2, y, dt):
             # norm1 + lrelu applied while conv2's halo conv stages its input: lrelu(norm1(y)) never reaches HBM
             y, st = _conv_gn(self.conv2, self.norm2, y, dt, cache, stream,
                              in_gn=(_gn_affine_table(self.norm1, y, st, stream), 0.2))
         else:
-            h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st)
+            h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st, split=split)
             y, st = _conv_gn(self.conv2, self.norm2, h, dt, cache, stream)
         pool = y.h > 1 and y.w > 1
-        return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st)
+        return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st, split=split)
 
     def forward_train_nhwc(self, h, dt):
         """Autograd path of run_nhwc: (NHWC activation, valid channels) -> the same after the block."""
@@ -336,10 +398,11 @@ class VGGBlock(nn.Module):
         return h, c
 
     def forward(self, x):
-        nv.forbid_autograd("VGGBlock.forward", (x,), (self,))
+        xin = x
         x = _check_input(x)
         stream = nv.stream_of(x)
-        return _to_nchw(self.run_nhwc(_to_nhwc(x, torch.float32, stream), torch.float32, self._cache, stream), stream)
+        y = _to_nchw(self.run_nhwc(_to_nhwc(x, torch.float32, stream), torch.float32, self._cache, stream), stream)
+        return nv.refuse_backward("VGGBlock.forward", y, (xin,), (self,))
 
 
 def _fresh_linear(in_features, out_features, device):
@@ -396,14 +459,14 @@ class HierarchyProjector(nn.Module):
         return mean + eps * std, mean, logvar
 
     def forward(self, x):
-        nv.forbid_autograd("HierarchyProjector.forward", (x,), (self,))
+        xin = x
         x = _check_input(x)
         stream = nv.stream_of(x)
         n = x.shape[0]
         pooled = _gap(_to_nhwc(x, torch.float32, stream), stream).contiguous()
         outs = [torch.empty([n, self.num_ws, self.w_dim], dtype=torch.float32, device=x.device) for _ in range(3)]
         self.run_pooled(pooled, outs, 0, self.num_ws, stream)
-        return tuple(outs)
+        return nv.refuse_backward("HierarchyProjector.forward", tuple(outs), (xin,), (self,))
 
 
 # ================================================================================================

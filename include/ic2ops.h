@@ -9,6 +9,12 @@
  *   - return IC2_OK (0) or an IC2_E_* code; ic2_last_error() returns the thread-local message;
  *   - dtype codes: IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 (f16 only where an entry point says so).  Activations on the synthesis path are NHWC with a
  *     channel stride padded to a multiple of 32 ("c_p"); padded channels hold zeros.
+ *   - IC2_BF16X3 = 3 (split bf16, only where an entry point says so): an f32 value v stored as hi = bf16(v),
+ *     lo = bf16(v - hi).  An NHWC activation of logical stride c_p is laid out as 3 * c_p bf16 channels per pixel,
+ *     [hi | hi | lo]; a packed weight as [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi].  A plain bf16 ic2_conv_igemm
+ *     over cin_p' = 3 * cin_p then accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi in f32: the product to ~2^-16
+ *     relative (the dropped x_lo*w_lo term is ~2^-18) at three bf16 MFMAs -- the encoder's parity mode that keeps
+ *     the 8-bit latent indices of the fp32 reference.
  *
  * The reference has no native code and no C ABI: each entry point names the Python
  * function of the reference (or of the un-vendored NVlabs/stylegan3 ops it calls) that it replaces.
@@ -24,7 +30,7 @@ extern "C" {
 #endif
 
 enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
-enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 };
+enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2, IC2_BF16X3 = 3 };
 enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
 /* NHWC16: channel-blocked NHWC, [n][c_p / 16][h][w][16] (the synthesis conv -> fused filtered lrelu hand-off) */
 enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1, IC2_LAYOUT_NHWC16 = 2 };
@@ -60,6 +66,14 @@ int ic2_codebook_lookup(const int64_t* codes, int64_t n, const float* codebook, 
 int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k, const float* log_tau,
                                 float tau, int hard, uint64_t seed, uint64_t offset, const float* gumbel_noise,
                                 float* disc_out, int64_t* idx_out, float* prob_sum_out, void* stream);
+
+/* Per-batch code record (SURVEY.md 8e metric record; usage / perplexity over the batch,
+ * gumbel_softmax_compression.py:121-127): kind 0 = f32 latents from ic2_quantize_uniform at `bits` (code =
+ * round((q + 1) * 0.5 * (2^bits - 1)), k = 2^bits), kind 1 = int64 codebook indices (k codes).  counts uint32 [k + 2],
+ * zeroed by the caller: += hist[0 .. k), codes outside [0, k) in counts[k], elements differing from golden (nullable,
+ * same kind; bitwise for kind 0) in counts[k + 1]. */
+int ic2_code_record(const void* codes, int kind, int k, int bits, const void* golden, int64_t n, uint32_t* counts,
+                    void* stream);
 
 /* ------------------------------------------- StyleGAN3 ops (torch_utils/ops, NVlabs/stylegan3) ---- */
 
@@ -116,7 +130,8 @@ int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y
            float w_gain, float b_gain, int act, float alpha, float act_gain, void* stream);
 
 /* Weight packing for the implicit GEMM: w[cout][cin][kh][kw] f32 -> w_out[cout_p][kh][kw][cin_p]
- * (dtype) times `scale`, zero padded.  prenorm != 0 applies modulated_conv2d's w * rsqrt(mean(w^2,[1,2,3]))
+ * (dtype) times `scale`, zero padded; dtype IC2_BF16X3 -> w_out[cout_p][kh][kw][3 * cin_p] bf16 = [hi | lo | hi].
+ * prenorm != 0 applies modulated_conv2d's w * rsqrt(mean(w^2,[1,2,3]))
  * and writes wsq_out[cout][cin] = sum_k w_norm^2 (nullable).  Called once per weight version. */
 int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
                     float scale, void* w_out, int dtype, float* wsq_out, void* stream);
@@ -140,6 +155,15 @@ int ic2_modconv_prep(const float* styles, const float* wsq, int n, int cin, int 
  * SynthesisLayer.forward [SG3-public] at the call site SynthesisNetwork.forward (stylegan3_hvae_full.py:274,329). */
 int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int w_dim, int nl, const int64_t* layers,
                              void* stream);
+
+/* The kernel instance(s) ic2_conv_igemm_ws launches for a geometry (its launch plan; host-only, no GPU needed),
+ * e.g. "igemm8_og2", "hg4_o128_w32_hb", "hconv_64_64", "torgb", "igemm_128x128_splitk".  Static storage. */
+const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, int n, int h, int w, int cin_p, int cout_p,
+                          int cout_valid, int kh, int kw, int pad);
+
+/* Non-zero when IC2_DEV=1: the development knobs (forced kernel instances, A/B switches; IC2_HG4, IC2_IGEMM_TILE,
+ * ...) are read from the environment only then -- otherwise the launch plan never depends on it. */
+int ic2_dev_mode(void);
 
 /* NHWC implicit-GEMM convolution on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32):
  *   acc[n,p,o] = sum_{ky,kx,i} w[o][ky][kx][i] * x[n, p + (ky,kx) - pad, i]   (zero outside the image)
@@ -174,13 +198,19 @@ int ic2_synth_input_features(const float* t, const float* freqs, const float* ph
 /* ------------------------------------------------------------------ encoder (HVAE_VGG) ---- */
 
 /* NCHW f32 -> NHWC (dtype) with channel stride c_p (zero padded), optionally times scale[n][c_p]
- * (nullable; a modulated layer's input scaling); the encoder's input packing. */
+ * (nullable; a modulated layer's input scaling); the encoder's input packing.  dtype IC2_BF16X3: 3 * c_p channels. */
 /* HVAE_VGG_Encoder.from_rgb (nn.Conv2d(cin, cout, 3, padding=1), stylegan3_hvae_full.py:62,175) read straight
  * from the NCHW f32 image: x [n][cin][h][w] f32 (cin <= 4, rounded to bf16 as ic2_nchw_to_nhwc does), w packed
  * bf16 [cout_p][3][3][cin_p] (ic2_pack_weight), bias [cout_p] f32 -> y bf16 NHWC [n][h][w][cout_p], cout_p in
  * {32, 64}.  Equals ic2_nchw_to_nhwc + ic2_conv_igemm (bf16) up to f32 summation order. */
 int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin_p, const float* bias, void* y, int n, int h,
                       int w_, int cout_p, void* stream);
+
+/* The same from_rgb in the encoder's split-bf16 mode: x f32 NCHW (not rounded), w the nn.Conv2d weight as is
+ * (f32 [cout][cin][3][3]), bias [cout_p] f32; exact f32 FMAs (tap order) -> y IC2_BF16X3 NHWC [n][h][w][3 * cout_p]
+ * ([hi | hi | lo], the input layout of the next split-bf16 conv).  cin <= 4, cout <= cout_p, cout_p in {32, 64, 128}. */
+int ic2_from_rgb_conv_x3(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n, int h,
+                         int w_, int cout_p, void* stream);
 
 int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c, int h, int w, int c_p, const float* scale,
                      void* stream);
@@ -197,13 +227,14 @@ int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c
                          float* stats_out, void* stream);
 
 /* GroupNorm apply + F.leaky_relu(0.2) (+ AvgPool2d(2,2) when pool != 0), VGGBlock.forward :183-191:
- *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling). */
+ *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling).  dtype_out may be
+ *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][3 * c_p]). */
 int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p, int c,
                       int groups, const float* stats, const float* gamma, const float* beta, float slope,
                       int pool, void* stream);
 
-/* AdaptiveAvgPool2d(1) of HierarchyProjector (:218): out [n][c] f32 = mean over H x W (NHWC input);
- * `out` is followed by scratch: ic2_global_avg_pool_floats() floats in total. */
+/* AdaptiveAvgPool2d(1) of HierarchyProjector (:218): out [n][c] f32 = mean over H x W (NHWC input; dtype
+ * IC2_BF16X3 sums hi + lo); `out` is followed by scratch: ic2_global_avg_pool_floats() floats in total. */
 int64_t ic2_global_avg_pool_floats(int n, int hw, int c_p, int c);
 int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int c_p, int c, float* out, void* stream);
 

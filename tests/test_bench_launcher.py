@@ -47,6 +47,15 @@ def test_self_launch_dry_run(world, tmp_path):
     for r in range(world):
         assert rec["rank_input_checksums"][r] == pytest.approx(_expected_checksum(r, 4), abs=1e-4)
     assert rec["scaling"] == "weak" and rec["higher_is_better"] is True
+    # the 8-bit code histogram of the metric record is summed over the ranks: every rank's codes
+    # counted once, the bins equal the sum of the per-rank histograms
+    mr = rec["metric_record"]
+    assert mr["hist_sum"] == world * 4 * 3 * 16 * 16 == mr["codes"]
+    from oracle import encoder as oe
+    hist = sum(torch.bincount(oe.uniform_indices(torch.rand(4, 3, 16, 16, generator=torch.Generator().manual_seed(
+        1000 + r)) * 2 - 1, 8).reshape(-1).clamp(0, 255), minlength=256).double() for r in range(world))
+    p = hist / hist.sum()
+    assert mr["code_perplexity"] == pytest.approx(float(torch.exp(-(p * torch.log(p + 1e-10)).sum())), abs=2e-3)
 
 
 def test_single_rank_dry_run():

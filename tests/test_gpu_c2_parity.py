@@ -1,5 +1,6 @@
-"""Parity of the BENCHED mode: the exact C2 workload (BASELINE.json configs[1]) -- batch 32, 256^2, bf16
-HVAE_VGG_Encoder(img_resolution=1024) -> 8-bit uniform quantizer -> SG3-T-256 synthesis -- against the oracle.
+"""Parity of the BENCHED mode: the exact C2 workload (BASELINE.json configs[1]) -- batch 32, 256^2,
+HVAE_VGG_Encoder(img_resolution=1024) -> 8-bit uniform quantizer -> SG3-T-256 synthesis, in bench.py's default
+precisions (encoder split-bf16 'bf16x3', synthesis bf16) -- against the oracle.
 
 Reference path: stylegan3_hvae_full.py:295-329 (compress -> decompress), metric hvae_training.py:368-395.
 The fp32 oracle means come from oracle/encoder.py (pinned to the reference's own encoder by
@@ -7,13 +8,15 @@ tests/golden/encoder_full.npz); the reference reconstruction is the fp32 path on
 latents (pinned to the CPU synthesis restatement at 1e-3 by test_gpu_path.py, re-checked here on 2 images).
 
 What is asserted (thresholds are module constants, measured values are printed and recorded in DESIGN.md (c)):
-  (a) quantized indices: the bf16 encoder's means stay within ENC_TOL of the oracle's; every index mismatch
-      is +-1 and lies within that distance of a half-step; the mismatch fraction is below IDX_FRAC;
+  (a) quantized indices (north star: bit-exact): the benched encoder's means within ENC_TOL of the oracle's;
+      at most IDX_FRAC of the 8-bit indices differ, each by one and only where the oracle latent lies within
+      HALF_STEP of a rounding boundary (the fp32 oracle's own reduction-order noise is ~1e-6 there);
   (b) reconstruction: signal-to-error of the bf16 image against the reference reconstruction, synthesis only
-      (same latents) and end to end (bf16 latents), above SNR_FLOOR_SYN / SNR_FLOOR_E2E;
-  (c) the north-star PSNR bar: |PSNR(bf16, target) - PSNR(reference, target)| below PSNR_TOL at a target
+      (same latents) and end to end (benched latents), above SNR_FLOOR_SYN / SNR_FLOOR_E2E;
+  (c) the north-star PSNR bar: |PSNR(bench, target) - PSNR(reference, target)| below PSNR_TOL at a target
       where PSNR is sensitive (reference reconstruction + Gaussian noise at the README's 34 dB operating
-      point), and reported at 46 dB.
+      point), and at 46 dB.
+The all-bf16 encoder (bench --precision bf16-all) is measured alongside and reported, not asserted.
 The perturbation test shows (b) can fail: one bf16-ulp (2^-8) error in every layer's filtered-lrelu gain
 or up-filter taps drops the SNR below the floor.
 """
@@ -29,13 +32,15 @@ from oracle import sg3
 pytestmark = pytest.mark.gpu
 
 B = 32
-# thresholds (measured on MI355X, round 2: max|dm| 2.38e-3, 4.6 % of indices off by one, synthesis-only SNR
-# 41.5 dB, end-to-end 38.8 dB, PSNR deltas -0.0045 / -0.0085 dB at 34 dB; one-ulp perturbations 24.3 / 31.7 dB)
-ENC_TOL = 4e-3          # max |means_bf16 - means_oracle| (latent units; the 8-bit step is 2/255 = 0.0078)
-IDX_FRAC = 0.08         # fraction of the 8-bit indices that may differ (by one) from the oracle's
+# thresholds.  Round 2 (all-bf16 encoder) measured max|dm| 2.4e-3 and 4.6 % of the indices off by one; the split-bf16
+# encoder is emulated on the CPU at max|dm| 3.5e-6, 1 flip in 32768 at 1.4e-6 from a half-step
+ENC_TOL = 5e-5          # max |means_bench - means_oracle| (latent units; the 8-bit step is 2/255 = 0.0078)
+IDX_FRAC = 1e-3         # fraction of the 8-bit indices that may differ (by one) from the oracle's
+HALF_STEP = 1e-4        # a differing index's oracle latent lies within this of a rounding boundary
 SNR_FLOOR_SYN = 38.0    # dB, bf16 synthesis vs the fp32 reference on identical latents
-SNR_FLOOR_E2E = 35.0    # dB, bf16 encode + quantize + synthesis vs the reference reconstruction
-PSNR_TOL = 0.01         # dB at the 34 dB operating point: the north-star bar
+SNR_FLOOR_E2E = 38.0    # dB, benched encode + quantize + synthesis vs the reference reconstruction
+PSNR_TOL = 0.005        # dB at the 34 dB operating point, end to end (north star: 0.01)
+PSNR_TOL_46 = 0.01      # dB at 46 dB
 
 
 def _snr_db(a, ref):
@@ -45,8 +50,10 @@ def _snr_db(a, ref):
 
 @pytest.fixture(scope="module")
 def c2(cuda):
+    import bench
+    enc_prec, syn_prec = bench.PRECISIONS["bf16"]   # the bench's default mode is the one tested here
     torch.manual_seed(0)
-    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision="bf16").to(cuda).eval().requires_grad_(False)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
     torch.manual_seed(1)
     G = ic2.Generator(img_resolution=256).to(cuda).eval().requires_grad_(False)
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1000)) * 2 - 1
@@ -54,18 +61,22 @@ def c2(cuda):
         torch.manual_seed(5)  # the fine projector re-draws fc1 from the CPU RNG (ref :225-230)
         _, m16, _ = enc(x.to(cuda))
         fc1 = (enc.fine_projector.fc1.weight.detach().cpu(), enc.fine_projector.fc1.bias.detach().cpu())
+        enc.set_precision("bf16")
+        torch.manual_seed(5)
+        _, m_allbf16, _ = enc(x.to(cuda))
+        enc.set_precision(enc_prec)
         sd = {k: v.detach().cpu() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
         _, m_or, _ = oe.encoder_forward(sd, x, fine_fc1=fc1)
         q16, i16 = ic2.quantize_uniform(m16, 8, return_indices=True)
         q_or = oe.quantize_uniform(m_or, 8)
         G.set_precision("fp32")
         ref = G.synthesis(q_or.to(cuda))
-        G.set_precision("bf16")
+        G.set_precision(syn_prec)
         img_e2e = G.synthesis(q16)
         img_syn = G.synthesis(q_or.to(cuda))
         G.set_precision("fp32")
     return dict(enc=enc, G=G, x=x, m16=m16.cpu(), m_or=m_or, i16=i16.cpu().long(), q_or=q_or, ref=ref,
-                img_e2e=img_e2e, img_syn=img_syn)
+                img_e2e=img_e2e, img_syn=img_syn, m_allbf16=m_allbf16.cpu())
 
 
 def test_c2_reference_reconstruction_is_the_oracle(c2):
@@ -77,24 +88,32 @@ def test_c2_reference_reconstruction_is_the_oracle(c2):
     assert err < 1e-3
 
 
-def test_c2_bf16_indices_vs_oracle(c2):
-    m16, m_or = c2["m16"], c2["m_or"]
-    err = (m16 - m_or).abs()
+def _index_stats(m, m_or):
+    err = (m - m_or).abs()
     i_or = oe.uniform_indices(m_or, 8)
-    d = c2["i16"] - i_or
+    d = oe.uniform_indices(m, 8) - i_or
     mism = d != 0
-    frac = mism.float().mean().item()
-    # distance of each mismatched oracle latent to the nearest half-step boundary of the 8-bit grid
+    # distance of each mismatched oracle latent to the nearest rounding boundary of the 8-bit grid
     u = (m_or.double() + 1) * 0.5 * 255
     dist = ((u - u.floor() - 0.5).abs() * 2 / 255)[mism]
-    print(f"[c2] encoder bf16 vs oracle: max|dm| = {err.max().item():.3e}, mean|dm| = {err.mean().item():.3e}, "
-          f"index mismatches {int(mism.sum())}/{mism.numel()} = {frac:.4f}, max |didx| = {int(d.abs().max())}, "
+    return err, d, mism, dist
+
+
+def test_c2_bench_indices_vs_oracle(c2):
+    m16, m_or = c2["m16"], c2["m_or"]
+    err, d, mism, dist = _index_stats(m16, m_or)
+    assert torch.equal(oe.uniform_indices(m16, 8), c2["i16"])   # the kernel's indices = the closed form
+    frac = mism.float().mean().item()
+    print(f"[c2] encoder (bench mode) vs oracle: max|dm| = {err.max().item():.3e}, mean|dm| = {err.mean().item():.3e}, "
+          f"index mismatches {int(mism.sum())}/{mism.numel()} = {frac:.2e}, max |didx| = {int(d.abs().max())}, "
           f"max half-step distance of a mismatch = {dist.max().item() if dist.numel() else 0.0:.3e}")
+    e2, d2, mism2, dist2 = _index_stats(c2["m_allbf16"], m_or)
+    print(f"[c2] all-bf16 encoder (reported): max|dm| = {e2.max().item():.3e}, index mismatches "
+          f"{int(mism2.sum())}/{mism2.numel()} = {mism2.float().mean().item():.2e}")
     assert err.max().item() < ENC_TOL
     assert d.abs().max().item() <= 1
-    if dist.numel():
-        assert (dist <= err[mism].double() + 1e-7).all()
-    assert frac < IDX_FRAC
+    assert frac <= IDX_FRAC
+    assert (dist <= HALF_STEP).all()
 
 
 def test_c2_bf16_reconstruction_snr(c2):

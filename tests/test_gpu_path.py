@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _inference():
-    """Inference tests: the HIP forwards refuse to run with grad required (nv.forbid_autograd)."""
+    """Inference tests run without a graph (grad mode works too: see test_gpu_path.py::test_grad_mode_inference)."""
     with torch.no_grad():
         yield
 
@@ -194,11 +194,13 @@ def test_encoder_small_matches_reference(cuda, golden_dir):
     assert enc.fine_projector.fc1.weight.shape == (256, 16)
 
 
-def test_encoder_full_config_matches_reference(cuda, golden_dir):
-    """HVAE_VGG_Encoder(img_resolution=1024) at seed 0 on 256^2 input (seed 1): reference latents."""
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_encoder_full_config_matches_reference(cuda, golden_dir, precision):
+    """HVAE_VGG_Encoder(img_resolution=1024) at seed 0 on 256^2 input (seed 1): reference latents, in the fp32
+    parity mode and in the benched split-bf16 mode (same bars: fp32-level latents, index-exact but at half-steps)."""
     d = np.load(os.path.join(golden_dir, "encoder_full.npz"))
     torch.manual_seed(0)
-    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024).to(cuda)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=precision).to(cuda)
     x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(1)) * 2 - 1
     w, m, lv = enc(x.to(cuda))
     ref_m = torch.from_numpy(d["means"])
@@ -229,6 +231,28 @@ def test_encoder_bf16_close_to_fp32(cuda):
     torch.manual_seed(3)
     _, m16, _ = enc(x)
     assert _maxdiff(m16[:, :12], m32[:, :12]) < 0.05 * (1 + m32.abs().max().item())
+
+
+def test_grad_mode_inference(cuda):
+    """Inference in grad mode: an unfrozen generator and the Gumbel discretization (learnable
+    temperature) run their HIP forwards and give the no-grad results; only .backward() through them raises."""
+    torch.manual_seed(21)
+    G = ic2.Generator(img_resolution=256).to(cuda)      # parameters require grad
+    ws = torch.randn(1, 16, 512, generator=torch.Generator().manual_seed(22)).to(cuda)
+    with torch.enable_grad():
+        img = G.synthesis(ws)
+        assert img.requires_grad
+        with pytest.raises(nv.AutogradUnsupported):
+            img.sum().backward()
+    with torch.no_grad():
+        assert torch.equal(img.detach(), G.synthesis(ws))
+    disc = ic2.GumbelSoftmaxDiscretization(512, 256).to(cuda).eval()
+    z = torch.rand(2, 16, 512, generator=torch.Generator().manual_seed(23)).to(cuda) * 2 - 1
+    with torch.enable_grad():
+        d, perp, idx = disc(z, hard=True)
+        assert torch.equal(idx.cpu(), oe.codebook_argmin(z.cpu()))
+        with pytest.raises(nv.AutogradUnsupported):
+            d.sum().backward()
 
 
 # ------------------------------------------------------------------ compressor API end to end

@@ -1,0 +1,122 @@
+"""The default launch plan picks only instances that a parity check here has run.
+
+The benched workloads (bench.py C2 / C2g / C4, --precision bf16 and bf16-all) are run once with bench.CallTimer
+recording every conv call; ic2_conv_plan (the dispatcher's own plan function) names the kernel instance of each.
+For every distinct instance one of its own geometries (the batch reduced while the plan keeps the instance) is run
+under the default plan and compared with the library's exact-fp32 MFMA conv (v_mfma_f32_16x16x4_f32, pinned to fp64
+by test_gpu_kernels.py::test_conv_igemm[float32]) on the same bf16 operands: the two differ only in f32 summation
+order.  Reference: the convs of HVAE_VGG_Encoder (stylegan3_hvae_full.py:62,175-176) and SG3 modulated_conv2d.
+"""
+import pytest
+import torch
+
+import bench
+import image_compression_2_amd as ic2
+from image_compression_2_amd import _native as nv
+
+pytestmark = pytest.mark.gpu
+
+
+def _record(cuda, res, gen_res, batch, enc_prec):
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=gen_res, precision="bf16").to(cuda).eval().requires_grad_(False)
+    comp = ic2.StyleGAN3Compressor(enc, G)
+    x = torch.rand(batch, 3, res, res, generator=torch.Generator().manual_seed(3)).to(cuda) * 2 - 1
+    timer = bench.CallTimer(nv, bench.CONV_ENTRIES)
+    timer.install()
+    timer.enabled = True
+    try:
+        with torch.no_grad():
+            comp.decompress(comp.compress(x))
+    finally:
+        timer.enabled = False
+        timer.uninstall()
+    return [(n, a) for n, a, _, _ in timer.calls(bench.CONV_ENTRIES)]
+
+
+def _geometry(name, a):
+    if name == "ic2_conv_igemm_ws":
+        dt, odt, n, h, w, cin_p, cout_p, cv, kh, kw, pad = a[3:14]
+        return dict(dt=dt, odt=odt, layout=a[23], n=n, h=h, w=w, cin_p=cin_p, cout_p=cout_p, cv=cv, kh=kh, kw=kw,
+                    pad=pad)
+    if name == "ic2_conv3x3_gn_fwd":
+        n, h, w, cin_p, cout_p, cv, kh, kw, pad = a[4:13]
+        return dict(dt=a[3], odt=a[3], layout=nv.NHWC, n=n, h=h, w=w, cin_p=cin_p, cout_p=cout_p, cv=cv, kh=kh, kw=kw,
+                    pad=pad)
+    return None   # from_rgb: its own kernels, test_gpu_kernels.py / test_gpu_split.py
+
+
+def _plan(g, n=None):
+    return nv.conv_plan(g["dt"], g["odt"], g["layout"], n or g["n"], g["h"], g["w"], g["cin_p"], g["cout_p"], g["cv"],
+                        g["kh"], g["kw"], g["pad"])
+
+
+@pytest.fixture(scope="module")
+def default_plan_instances(cuda):
+    inst = {}
+    for res, gen_res, batch in ((256, 256, 32), (1024, 1024, 8)):
+        for enc_prec in ("bf16x3", "bf16"):
+            if res == 1024 and enc_prec == "bf16":
+                continue
+            for name, a in _record(cuda, res, gen_res, batch, enc_prec):
+                g = _geometry(name, a)
+                if g is None:
+                    continue
+                p = _plan(g)
+                m = g["n"] * g["h"] * g["w"]
+                if p not in inst or m < inst[p]["n"] * inst[p]["h"] * inst[p]["w"]:
+                    inst[p] = g
+    return inst
+
+
+def test_default_plan_instances_listed(default_plan_instances):
+    names = sorted(default_plan_instances)
+    print("[plan] instances on the benched workloads:", names)
+    assert "igemm8_og2" in names and any(n.startswith("hg4_") for n in names)
+
+
+def _run_conv(g, n, cuda, dt_in):
+    gen = torch.Generator().manual_seed(n * 7 + g["cin_p"])
+    ho, wo = g["h"] + 2 * g["pad"] - g["kh"] + 1, g["w"] + 2 * g["pad"] - g["kw"] + 1
+    x = (torch.randn(n, g["h"], g["w"], g["cin_p"], generator=gen)).to(torch.bfloat16)
+    w = (torch.randn(g["cout_p"], g["kh"], g["kw"], g["cin_p"], generator=gen) /
+         (g["kh"] * g["kw"] * g["cin_p"]) ** 0.5).to(torch.bfloat16)
+    w[g["cv"]:] = 0
+    bias = torch.randn(g["cout_p"], generator=gen) * 0.1
+    outs = []
+    for dt, odt, layout in ((nv.BF16, g["odt"], g["layout"]), (nv.F32, nv.F32, nv.NHWC)):
+        tdt = torch.bfloat16 if dt == nv.BF16 else torch.float32
+        xd, wd, bd = x.to(tdt).to(cuda), w.to(tdt).to(cuda), bias.to(cuda)
+        if layout == nv.NCHW:
+            y = torch.empty(n, g["cv"], ho, wo, dtype=torch.float32, device=cuda)
+        elif layout == nv.NHWC16:
+            y = torch.empty(n, g["cout_p"] // 16, ho, wo, 16, dtype=torch.float16 if odt == nv.F16 else torch.bfloat16,
+                            device=cuda)
+        else:
+            y = torch.empty(n, ho, wo, g["cout_p"], dtype={nv.F32: torch.float32, nv.BF16: torch.bfloat16,
+                                                           nv.F16: torch.float16}[odt], device=cuda)
+        nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), dt, odt, n, g["h"], g["w"], g["cin_p"], g["cout_p"], g["cv"],
+                      g["kh"], g["kw"], g["pad"], ho, wo, None, nv.ptr(bd), 0, 0.0, 1.0, -1.0, 1.0, layout, nv.stream_of(xd),
+                      cuda)
+        torch.cuda.synchronize()
+        if layout == nv.NCHW:
+            y = y.permute(0, 2, 3, 1)
+        elif layout == nv.NHWC16:
+            y = y.permute(0, 2, 3, 1, 4).reshape(n, ho, wo, g["cout_p"])
+        outs.append(y[..., :g["cv"]].float().cpu())
+    return outs
+
+
+def test_every_default_plan_instance_matches_fp32(cuda, default_plan_instances):
+    for p, g in sorted(default_plan_instances.items()):
+        n = 1
+        while _plan(g, n) != p and n < g["n"]:
+            n += 1
+        assert _plan(g, n) == p
+        got, ref = _run_conv(g, n, cuda, nv.BF16)
+        tol = (2e-3 if g["odt"] != nv.F32 else 1e-4) * (1 + ref.abs().max().item())
+        err = (got - ref).abs().max().item()
+        print(f"[plan] {p}: n={n} {g['h']}x{g['w']} {g['cin_p']}->{g['cout_p']} max|err| {err:.2e}")
+        assert err < tol, p

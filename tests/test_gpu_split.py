@@ -1,0 +1,161 @@
+"""The encoder's split-bf16 mode (precision='bf16x3', ic2ops.h IC2_BF16X3), op by op against fp64.
+
+Each f32 operand v is carried as hi = bf16(v), lo = bf16(v - hi); a conv accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi
+in f32 on bf16 MFMAs (the tripled-K GEMM), so a product is exact to ~2^-16 relative.  Reference functions:
+VGGBlock.forward / HVAE_VGG_Encoder.forward, stylegan3_hvae_full.py:105-191.  The end-to-end bar (8-bit indices of
+the fp32 reference) is tests/test_gpu_c2_parity.py and test_gpu_path.py::test_encoder_full_config_matches_reference.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from image_compression_2_amd import _native as nv
+from image_compression_2_amd import stylegan3_hvae_full as shf
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _inference():
+    with torch.no_grad():
+        yield
+
+
+def _split_pack(x, cuda):
+    """NCHW f32 -> split-bf16 NHWC activation handle (ic2_nchw_to_nhwc, dtype IC2_BF16X3)."""
+    n, c, h, w = x.shape
+    c_p = nv.pad32(c)
+    xd = x.to(cuda).contiguous()
+    t = torch.empty([n, h, w, 3 * c_p], dtype=torch.bfloat16, device=cuda)
+    nv.call("ic2_nchw_to_nhwc", nv.ptr(xd), nv.ptr(t), nv.BF16X3, n, c, h, w, c_p, None, nv.stream_of(xd))
+    torch.cuda.synchronize()
+    return shf._Act(t, c, x3=True)
+
+
+def _unsplit(a):
+    """split activation -> NCHW f32 (hi + lo) of its c logical channels; also checks the [hi | hi | lo] layout."""
+    t = a.t.float().cpu()
+    cp = a.c_p
+    hi, hi2, lo = t[..., :cp], t[..., cp:2 * cp], t[..., 2 * cp:]
+    assert torch.equal(hi, hi2)
+    return (hi.double() + lo.double())[..., :a.c].permute(0, 3, 1, 2)
+
+
+def test_split_packing_is_hi_lo(cuda):
+    x = torch.randn(2, 5, 7, 9, generator=torch.Generator().manual_seed(1)) * 3
+    a = _split_pack(x, cuda)
+    t = a.t.float().cpu()
+    hi = x.to(torch.bfloat16).float().permute(0, 2, 3, 1)
+    lo = (x - x.to(torch.bfloat16).float()).to(torch.bfloat16).float().permute(0, 2, 3, 1)
+    assert torch.equal(t[..., :5], hi) and torch.equal(t[..., 64:69], lo)
+    assert (t[..., 5:32] == 0).all() and (t[..., 69:] == 0).all()
+    assert (_unsplit(a) - x.double()).abs().max().item() <= 2 ** -16 * x.abs().max().item()
+
+
+def test_split_weight_packing(cuda):
+    conv = torch.nn.Conv2d(40, 20, 3, padding=1)
+    a = shf._Act(torch.zeros(1, 4, 4, 3 * 64, dtype=torch.bfloat16, device=cuda), 40, x3=True)
+    wp, bp = shf._packed(conv.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
+    torch.cuda.synchronize()
+    assert wp.shape == (32, 3, 3, 192)
+    w = conv.weight.detach().cpu().permute(0, 2, 3, 1)  # [o][ky][kx][i]
+    hi = w.to(torch.bfloat16).float()
+    lo = (w - hi).to(torch.bfloat16).float()
+    got = wp.float().cpu()
+    assert torch.equal(got[:20, ..., :40], hi) and torch.equal(got[:20, ..., 64:104], lo)
+    assert torch.equal(got[:20, ..., 128:168], hi)
+    assert (got[20:] == 0).all() and (got[..., 40:64] == 0).all()
+
+
+# shapes reaching the launch plan's kernels at the tripled channel strides: hg4 (<= 256 in), the 8-phase
+# kernels (384 / 768 / 1536 in), the small-grid igemm with split-K (the 16^2 .. 2^2 encoder blocks)
+SPLIT_CONV_CASES = [(32, 64, 2, 150), (64, 64, 2, 129), (64, 128, 4, 64), (128, 128, 4, 64), (128, 256, 8, 32),
+                    (256, 512, 8, 16), (512, 512, 8, 8), (512, 512, 16, 2), (40, 20, 2, 33)]
+
+
+@pytest.mark.parametrize("cin,cout,n,size", SPLIT_CONV_CASES)
+def test_split_conv_gn_matches_fp64(cuda, cin, cout, n, size):
+    """_conv_gn in split mode: the f32 conv output within 2e-5 (relative to max |y|) of F.conv2d in fp64 on the
+    unrounded f32 operands (a plain bf16 conv: ~1e-2), and the GroupNorm statistics of that output."""
+    g = torch.Generator().manual_seed(cin * 7 + cout + size)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    norm = torch.nn.GroupNorm(min(32, cout), cout)
+    x = torch.randn(n, cin, size, size, generator=g)
+    a = _split_pack(x, cuda)
+    y, st = shf._conv_gn(conv.to(cuda), norm.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
+    torch.cuda.synchronize()
+    assert y.t.dtype == torch.float32 and not y.x3
+    r = F.conv2d(x.double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(), padding=1)
+    got = y.t[..., :cout].cpu().double().permute(0, 3, 1, 2)
+    err = (got - r).abs().max().item() / r.abs().max().item()
+    print(f"[split conv {cin}->{cout} n{n} {size}^2] max rel err {err:.2e}")
+    assert err < 2e-5
+    assert (y.t[..., cout:] == 0).all()
+    groups = norm.num_groups
+    rg = r.reshape(n, groups, -1)
+    mean, var = rg.mean(-1), rg.var(-1, unbiased=False)
+    s = st[: n * groups * 2].view(n, groups, 2).cpu().double()
+    assert torch.allclose(s[..., 0], mean, rtol=1e-4, atol=1e-5 * r.abs().max().item())
+    assert torch.allclose(s[..., 1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_split_gn_lrelu_pool(cuda, pool):
+    """GroupNorm + lrelu (+ pool) in f32, stored split: hi + lo within 2^-16 of the fp64 result."""
+    g = torch.Generator().manual_seed(3)
+    n, c, h, w = 3, 96, 18, 14
+    y = torch.randn(n, c, h, w, generator=g) * 2 + 0.3
+    norm = torch.nn.GroupNorm(32, c)
+    with torch.no_grad():
+        norm.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        norm.bias.copy_(torch.randn(c, generator=g))
+    stream = nv.stream_of()
+    ya = shf._to_nhwc(y.to(cuda), torch.float32, stream)
+    out = shf._group_norm_lrelu(norm.to(cuda), ya, pool, torch.bfloat16, stream, split=True)
+    assert out.x3 and out.t.shape[-1] == 3 * 96
+    r = F.leaky_relu(F.group_norm(y.double(), 32, norm.weight.detach().cpu().double(),
+                                  norm.bias.detach().cpu().double(), 1e-5), 0.2)
+    if pool:
+        r = F.avg_pool2d(r, 2)
+    got = _unsplit(out)
+    assert (got - r).abs().max().item() < 2e-6 * (1 + r.abs().max().item())
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(3, 32, 3, 67, 45), (3, 64, 2, 40, 33), (1, 32, 1, 9, 70), (3, 128, 2, 33, 40),
+                                             (3, 20, 2, 16, 32)])
+def test_from_rgb_split_exact(cuda, cin, cout, n, h, w):
+    """ic2_from_rgb_conv_x3: exact f32 FMAs on the unrounded image, stored split -> within 2^-16 of fp64."""
+    g = torch.Generator().manual_seed(cin * 100 + cout + h)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    x = torch.rand(n, cin, h, w, generator=g) * 2 - 1
+    a = shf._from_rgb(conv.to(cuda), x.to(cuda), torch.bfloat16, {}, nv.stream_of(), split=True)
+    torch.cuda.synchronize()
+    assert a.x3 and a.c == cout
+    r = F.conv2d(x.double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(), padding=1)
+    got = _unsplit(a)
+    assert (got - r).abs().max().item() < 1e-5 * (1 + r.abs().max().item())
+
+
+def test_from_rgb_split_generic_route(cuda):
+    """from_rgb shapes without the direct kernel (5x5 here) take an exact f32 conv + split packing."""
+    g = torch.Generator().manual_seed(9)
+    conv = torch.nn.Conv2d(3, 32, 5, padding=2)
+    x = torch.rand(2, 3, 21, 19, generator=g) * 2 - 1
+    a = shf._from_rgb(conv.to(cuda), x.to(cuda), torch.bfloat16, {}, nv.stream_of(), split=True)
+    r = F.conv2d(x.double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(), padding=2)
+    assert (_unsplit(a) - r).abs().max().item() < 1e-5 * (1 + r.abs().max().item())
+
+
+def test_split_global_avg_pool(cuda):
+    x = torch.randn(3, 40, 9, 11, generator=torch.Generator().manual_seed(2)) * 2
+    a = _split_pack(x, cuda)
+    got = shf._gap(a, nv.stream_of()).cpu().double()
+    r = x.double().mean((2, 3))
+    assert (got - r).abs().max().item() < 1e-5

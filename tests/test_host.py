@@ -87,31 +87,37 @@ def test_product_path_refuses_cpu_tensors():
         enc(torch.zeros(1, 3, 32, 32))
 
 
-def test_forwards_refuse_autograd():
-    """No silent loss of autograd (reference training loop stylegan3_hvae_full.py:669-696): with grad mode on
-    and a parameter or input requiring grad, every HIP forward raises before touching the device."""
+def test_grad_mode_forwards_reach_the_device_and_refuse_backward():
+    """Inference keeps working in grad mode: no forward refuses up front any more -- each one reaches the
+    device check (CPU tensors: no fallback) -- and a HIP forward without a backward returns outputs whose
+    .backward() raises AutogradUnsupported (nv.refuse_backward) instead of silently training nothing."""
     enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=256, channel_max=32, w_dim=32)
-    x = torch.zeros(1, 3, 32, 32)
     with pytest.raises(RuntimeError, match="ROCm"):
-        enc(x)   # the encoder trains through its HIP autograd path (autograd_ops); no CPU fallback either way
-    with pytest.raises(nv.AutogradUnsupported):
+        enc(torch.zeros(1, 3, 32, 32))   # the encoder trains through its HIP autograd path (autograd_ops)
+    with pytest.raises(RuntimeError, match="ROCm"):
         enc.blocks[0](torch.zeros(1, 32, 8, 8))
     G = ic2.Generator(img_resolution=256)
     ws = torch.zeros(1, 16, 512)
-    with pytest.raises(nv.AutogradUnsupported):
-        G.synthesis(ws)                          # parameters require grad
-    with pytest.raises(nv.AutogradUnsupported):
-        G.synthesis(ws.clone().requires_grad_(True))   # weight gradients are not implemented (G is frozen)
+    for w in (ws, ws.clone().requires_grad_(True)):
+        with pytest.raises(RuntimeError, match="ROCm"):
+            G.synthesis(w)               # unfrozen G: the inference path (its output refuses backward)
     G.requires_grad_(False)
     with pytest.raises(RuntimeError, match="ROCm"):
         G.synthesis(ws.clone().requires_grad_(True))   # frozen G, grads into W+: the HIP autograd path
-    with pytest.raises(RuntimeError, match="ROCm"):
-        G.synthesis(ws.detach())                 # frozen and no input grad: reaches the device check
     disc = ic2.GumbelSoftmaxDiscretization(32, 256)   # learnable temperature
+    with pytest.raises(RuntimeError, match="ROCm"):
+        disc(torch.zeros(1, 16, 32))
+    # the refusal node itself: pass-through in the forward (same storage), raise on backward, no-op without grad
+    p = torch.nn.Linear(2, 2)
+    out = torch.randn(4)
+    y, idx = nv.refuse_backward("t", (out, torch.arange(3)), (), (p,))
+    assert y.requires_grad and y.data_ptr() == out.data_ptr() and idx.dtype == torch.int64
     with pytest.raises(nv.AutogradUnsupported):
-        disc(torch.zeros(1, 16, 32))
-    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm"):
-        disc(torch.zeros(1, 16, 32))
+        y.sum().backward()
+    with torch.no_grad():
+        assert nv.refuse_backward("t", out, (), (p,)) is out
+    p.requires_grad_(False)
+    assert nv.refuse_backward("t", out, (torch.zeros(2),), (p,)) is out
 
 
 # ------------------------------------------------------------------ seeded construction = reference
@@ -181,3 +187,42 @@ def test_shard_partition(n, world):
         assert b == c and b >= a
     sizes = [b - a for a, b in spans]
     assert max(sizes) - min(sizes) <= 1
+
+
+# ------------------------------------------------------------------ launch plan (host-only query) + knob gating
+def test_conv_launch_plan_names():
+    """ic2_conv_plan is the dispatcher's own plan function (no GPU needed): the SG3-T-256 / encoder shapes of the
+    C2 workload land on the instances DESIGN.md lists."""
+    plan = lambda *a: nv.conv_plan(*a)
+    B = 32
+    # SG3-T-256 L8 (512 -> 512 at 148^2, f16 NHWC16 out): the 8-phase 256 x 256 kernel
+    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 148, 148, 512, 512, 512, 3, 3, 2) == "igemm8_og2"
+    # L9 (512 -> 362, cout_p 384): 256-wide + 128 x 512 launches
+    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 148, 148, 512, 384, 362, 3, 3, 2) == "igemm8_og2+og1"
+    # L11 (256 -> 181 at 276^2, cout_p 192): the 4-wave halo GEMM
+    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 276, 276, 256, 192, 181, 3, 3, 2).startswith("hg4_o192")
+    # ToRGB: the VALU 1x1 kernel
+    assert plan(nv.BF16, nv.F32, nv.NCHW, B, 256, 256, 128, 32, 3, 1, 1, 0) == "torgb"
+    # encoder block 0 conv2 in bf16 (64 -> 64 at 256^2): the halo direct conv; split-bf16 (192 tripled channels): hg4
+    assert plan(nv.BF16, nv.BF16, nv.NHWC, B, 256, 256, 64, 64, 64, 3, 3, 1) == "hconv_64_64"
+    assert plan(nv.BF16, nv.F32, nv.NHWC, B, 256, 256, 192, 64, 64, 3, 3, 1).startswith("hg4_o64")
+    # small late encoder blocks: split-K implicit GEMM; fp32 mode: the exact-f32 tile
+    assert plan(nv.BF16, nv.F32, nv.NHWC, B, 4, 4, 1536, 512, 512, 3, 3, 1).endswith("_splitk")
+    assert plan(nv.F32, nv.F32, nv.NHWC, 2, 16, 16, 64, 64, 64, 3, 3, 1).startswith("igemm_f32")
+
+
+def test_knobs_are_ignored_without_dev_mode():
+    """The development knobs (forced instances / A/B switches) change the launch plan only under IC2_DEV=1."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from image_compression_2_amd import _native as nv; "
+            "print(nv.conv_plan(nv.BF16, nv.F16, nv.NHWC16, 32, 148, 148, 512, 512, 512, 3, 3, 2), "
+            "nv.query('ic2_dev_mode'))" % ROOT)
+    outs = {}
+    for dev in ("0", "1"):
+        env = dict(os.environ, IC2_IGEMM_TILE="4", IC2_DEV=dev)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs[dev] = r.stdout.split()
+    assert outs["0"] == ["igemm8_og2", "0"]
+    assert outs["1"] == ["igemm_128x128", "1"]
