@@ -487,6 +487,10 @@ def run(args):
             return torch.cat([rec[N_CODES + 1:], rec[N_CODES:N_CODES + 1], rec[:N_CODES]]).double()
 
         def step():
+            # the fine projector re-draws its fc1 from the CPU generator on every call (reference quirk,
+            # stylegan3_hvae_full.py:225-230): a fixed seed per step makes that draw -- and so every code -- the same
+            # on every step and every rank (the record's index-mismatch count is then a determinism check)
+            torch.manual_seed(5)
             with torch.no_grad():
                 if args.config == "c2g":
                     codes = comp.compress_codes(x, discrete_bits=8)

@@ -26,8 +26,14 @@ from .gumbel_softmax_compression import GumbelSoftmaxDiscretization, check_codes
 
 _MAGIC = b"IC2R"
 _VERSION = 1
-_MAX_SYMBOLS_PER_STREAM = 1 << 24   # an untrusted header may not ask for more than this per image
+_MAX_SYMBOLS_PER_STREAM = 1 << 24   # an untrusted header may not ask for more than this per image ...
 _MAX_STREAMS = 1 << 16
+_MAX_TOTAL_SYMBOLS = 1 << 26        # ... nor for more than this in total (256 MiB of int32 codes)
+# The coder's probabilities saturate at 2017/2048 (11 bits, shift-5 update), so a binary decision costs >= 0.022
+# bits and a symbol (8 decisions) >= 0.176 bits: a stream cannot hold more than ~45 symbols per byte.  Its flush
+# writes 5 bytes, so a genuine stream is never shorter.
+_MAX_SYMBOLS_PER_BYTE = 64
+_MIN_STREAM_BYTES = 5
 
 
 class ContextModel:
@@ -76,8 +82,11 @@ def cabac_decode(encoded_bytes, context_model, shape=None):
     _, version, b, num_ws, w_dim, n_symbols = struct.unpack_from("<4s5I", buf, 0)
     if version != _VERSION:
         raise ValueError(f"unsupported IC2R version {version}")
-    # the header is untrusted: bound the allocation it asks for before making it
-    if not (0 < b <= _MAX_STREAMS and 0 < num_ws and 0 < w_dim and num_ws * w_dim <= _MAX_SYMBOLS_PER_STREAM):
+    # the header is untrusted: bound the allocation it asks for before making it -- per stream, in total, and by
+    # what the payload bytes can possibly decode to
+    per = num_ws * w_dim
+    if not (0 < b <= _MAX_STREAMS and 0 < num_ws and 0 < w_dim and per <= _MAX_SYMBOLS_PER_STREAM
+            and b * per <= _MAX_TOTAL_SYMBOLS):
         raise ValueError(f"implausible IC2R header: {b} streams of {num_ws} x {w_dim} symbols")
     if len(buf) < 24 + 4 * b:
         raise ValueError("truncated IC2R header")
@@ -87,6 +96,8 @@ def cabac_decode(encoded_bytes, context_model, shape=None):
         raise ValueError(f"stream shape {(b, num_ws, w_dim)} != expected {tuple(shape)}")
     off = 24 + 4 * b
     sizes = np.array(struct.unpack_from(f"<{b}I", buf, 24), dtype=np.int64)
+    if (sizes < _MIN_STREAM_BYTES).any() or (per > _MAX_SYMBOLS_PER_BYTE * sizes).any():
+        raise ValueError(f"implausible IC2R stream sizes for {per} symbols per stream")
     payload = np.frombuffer(buf, dtype=np.uint8, offset=off)
     if payload.size < int(sizes.sum()):
         raise ValueError("truncated IC2R stream")

@@ -1496,11 +1496,8 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
       else launch_hconv<96, 64>(a, s);
       break;
     case CK_IGEMM:
-      if (dtype != IC2_BF16) {
-        launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
-        break;
-      }
-      switch (pl.tile) {
+      if (dtype != IC2_BF16) launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
+      else switch (pl.tile) {
         case 6: launch_g8<2>(a, s); break;
         case 7:
           if (c.split384) {

@@ -95,7 +95,29 @@ def launch(world, fn, *args):
     device), each with torchrun's env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT),
     running fn(*args).  Raises if any rank fails."""
     import torch.multiprocessing as mp
-    mp.start_processes(_spawned, args=(world, free_port(), fn, args), nprocs=world, join=True, start_method="spawn")
+    # free_port() releases the port before rank 0's store binds it; if another process takes it in between, the
+    # rendezvous fails with "address already in use": retry on a fresh port (ADVICE r2)
+    for attempt in range(4):
+        try:
+            mp.start_processes(_spawned, args=(world, free_port(), fn, args), nprocs=world, join=True,
+                               start_method="spawn")
+            return
+        except Exception as e:  # torch.multiprocessing.ProcessRaisedException carries the rank's traceback text
+            msg = str(e).lower()
+            if attempt == 3 or not ("address already in use" in msg or "eaddrinuse" in msg):
+                raise
+
+
+def broadcast_params(module, src=0):
+    """Copy `module`'s parameters from rank `src` to every rank (in place; no-op when not distributed).  Used for
+    the fine projector's fc1, which the reference re-creates from each process's CPU generator on every call
+    (stylegan3_hvae_full.py:225-230): without it the ranks of a data-parallel step would run -- and average the
+    gradients of -- different weights."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    with torch.no_grad():
+        for p in module.parameters():
+            dist.broadcast(p.data, src)
 
 
 def barrier(device=None):

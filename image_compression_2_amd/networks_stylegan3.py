@@ -37,6 +37,8 @@ from . import sg3_ops
 # conv -> filtered lrelu hand-off in the channel-blocked NHWC16 layout (bf16 mode); knob IC2_FLR_BLOCKED=0 (IC2_DEV=1):
 # plain NHWC
 _FLR_BLOCKED = nv.knob("IC2_FLR_BLOCKED", 1) != 0
+# longest row (w_dim, cin) of ic2_modconv_prep_batched's LDS-staged small GEMM (synth_ops.hip kSmK)
+_MOD_BATCH_MAX = 512
 
 
 def _train_mode(module, *tensors):
@@ -332,13 +334,30 @@ class SynthesisLayer(torch.nn.Module):
                 self.out_channels, self.cout_p, int(not self.is_torgb), f32(fc.weight_gain), f32(fc.bias_gain),
                 f32(style_gain), f32(self.input_gain())]
 
-    def scales(self, ws, ldx, n, dt):
+    def batchable(self):
+        """Fits ic2_modconv_prep_batched's LDS-staged small GEMM (rows of <= 512: w_dim and cin)."""
+        return self.in_channels <= _MOD_BATCH_MAX and self.affine.in_features <= _MOD_BATCH_MAX
+
+    def scales(self, ws, ldx, n, dt, unbatched=False):
         """Runs the affine FC and the (de)modulation prep: -> (xscale [n][cin_p], oscale [n][cout_p]).
-        The same kernels as SynthesisNetwork.scales_batched (a one-layer batch), so both give identical bits."""
+        The same kernels as SynthesisNetwork.scales_batched (a one-layer batch), so both give identical bits; a
+        layer wider than that kernel's rows (channel_max > 512) -- or unbatched=True -- takes the
+        per-layer kernels ic2_fc + ic2_modconv_prep (no width cap)."""
         dev = ws.device
         styles = torch.empty([n, self.in_channels], dtype=torch.float32, device=dev)
         xs = torch.empty([n, self.cin_p], dtype=torch.float32, device=dev)
         os_ = torch.empty([n, self.cout_p], dtype=torch.float32, device=dev)
+        if unbatched or not self.batchable():
+            _, wsq, _ = self.packed(dt)
+            fc = self.affine
+            stream = nv.stream_of(ws)
+            nv.call("ic2_fc", nv.ptr(ws), ldx, nv.ptr(fc.weight), nv.ptr(fc.bias), nv.ptr(styles), n, fc.in_features,
+                    self.in_channels, float(fc.weight_gain), float(fc.bias_gain), nv.ACT_LINEAR, 0.0, 1.0, stream)
+            style_gain = float(1 / np.sqrt(self.in_channels * (self.conv_kernel ** 2))) if self.is_torgb else 1.0
+            nv.call("ic2_modconv_prep", nv.ptr(styles), nv.ptr(wsq), n, self.in_channels, self.out_channels,
+                    self.cin_p, self.cout_p, int(not self.is_torgb), style_gain, float(self.input_gain()), nv.ptr(xs),
+                    nv.ptr(os_), None, stream)
+            return xs, os_
         rec = np.asarray([self.mod_record(dt, 0, styles, xs, os_)], dtype=np.int64)
         nv.call("ic2_modconv_prep_batched", nv.ptr(ws), ldx, n, self.affine.in_features, 1,
                 rec.ctypes.data_as(ctypes.c_void_p), nv.stream_of(ws))
@@ -583,8 +602,12 @@ class SynthesisNetwork(torch.nn.Module):
         return _refuse(self, x, ws_in)
 
     def scales_batched(self, ws, ldx, n, dt):
-        """[(xscale [n][cin_p], oscale [n][cout_p]) per layer] through ic2_modconv_prep_batched."""
+        """[(xscale [n][cin_p], oscale [n][cout_p]) per layer] through ic2_modconv_prep_batched (per layer when a
+        layer is wider than its rows allow)."""
         layers = self.layers()
+        if not all(L.batchable() for L in layers):
+            flat = ws.view(-1)
+            return [L.scales(flat[(i + 1) * self.w_dim:], ldx, n, dt) for i, L in enumerate(layers)]
         sizes = [(n * L.in_channels + 3) // 4 * 4 + n * L.cin_p + n * L.cout_p for L in layers]
         buf = torch.empty([sum(sizes)], dtype=torch.float32, device=ws.device)
         rec = np.zeros([len(layers), 16], dtype=np.int64)

@@ -256,10 +256,16 @@ class HVAE_VGG_Encoder(nn.Module):
     """Full VGG-style HVAE encoder (ref ``stylegan3_hvae_full.py:29-167``)."""
 
     def __init__(self, img_resolution=1024, img_channels=3, w_dim=512, num_ws=16, block_split=(5, 12),
-                 channel_base=32768, channel_max=512, use_fp16=False, precision="fp32"):
-        """precision (extension, not in the reference): 'fp32' (parity, exact-f32 MFMA), 'bf16' (bf16 storage and
-        MFMA), 'bf16x3' (split bf16: three bf16 MFMA terms per product, f32 storage -- latents at fp32 level, the
-        8-bit indices of the fp32 reference)."""
+                 channel_base=32768, channel_max=512, use_fp16=False, precision="fp32", fix_fine_projector=False):
+        """Extensions (not in the reference), both opt-in:
+        precision: 'fp32' (parity, exact-f32 MFMA), 'bf16' (bf16 storage and MFMA), 'bf16x3' (split bf16: three bf16
+            MFMA terms per product, f32 storage -- latents at fp32 level, the 8-bit indices of the fp32 reference;
+            DESIGN.md (c)).
+        fix_fine_projector: the reference builds the fine projector's fc1 for 64 inputs, receives 128 and re-creates
+            fc1 with fresh random weights on every call (:225-230, SURVEY.md 5 bug 1).  True builds fc1 for the
+            pooled width once, right after the reference's construction (so every other weight is still drawn as the
+            reference draws it) and keeps it: slots 12-15 become deterministic and trainable, and data-parallel ranks
+            agree without broadcasting fc1."""
         super().__init__()
         self.img_resolution = img_resolution
         self.img_channels = img_channels
@@ -286,6 +292,16 @@ class HVAE_VGG_Encoder(nn.Module):
         self.global_projector = HierarchyProjector(channels[self.hierarchy_blocks["global"]], w_dim, self.num_ws_global)
         self.medium_projector = HierarchyProjector(channels[self.hierarchy_blocks["medium"]], w_dim, self.num_ws_medium)
         self.fine_projector = HierarchyProjector(channels[self.hierarchy_blocks["fine"]], w_dim, self.num_ws_fine)
+        self.fix_fine_projector = fix_fine_projector
+        if fix_fine_projector:
+            # the width the fine projector actually pools: the output of block `fine` (channels[fine + 1])
+            for proj, key in ((self.global_projector, "global"), (self.medium_projector, "medium"),
+                              (self.fine_projector, "fine")):
+                blk = self.hierarchy_blocks[key]
+                width = channels[blk + 1] if blk < self.num_layers - 1 else channels[blk]
+                if width != proj.in_channels:
+                    proj.fc1 = nn.Linear(width, 256)
+                    proj.in_channels = width
         self._cache = {}
 
     def set_precision(self, precision):
@@ -431,12 +447,20 @@ class HierarchyProjector(nn.Module):
         self.act = nn.LeakyReLU(0.2)
         self.fc2 = nn.Linear(256, num_ws * w_dim * 2)
 
+    fc1_hook = None   # callable(fc1) run after each re-creation (training.train_step: broadcast from rank 0)
+
+    def refresh_fc1(self, in_features, device):
+        """Reference quirk (:225-230): a fresh nn.Linear(in_features, 256) on EVERY call whose pooled width differs
+        from in_channels, drawn from the CPU generator; then the hook (data-parallel consistency)."""
+        self.fc1 = _fresh_linear(in_features, 256, device)
+        if self.fc1_hook is not None:
+            self.fc1_hook(self.fc1)
+
     def run_pooled(self, pooled, outs, off, ws_total, stream):
         """pooled [N, C] f32 -> writes slots [off, off + num_ws) of (w, mean, logvar)."""
         n, in_features = pooled.shape
         if in_features != self.in_channels:
-            # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
-            self.fc1 = _fresh_linear(in_features, 256, pooled.device)
+            self.refresh_fc1(in_features, pooled.device)
         h = _linear(self.fc1, pooled, stream, act=True, slope=self.act.negative_slope)
         p = _linear(self.fc2, h, stream)
         # torch.randn_like(std) on the device, in the reference's order (global, medium, fine)
@@ -449,8 +473,7 @@ class HierarchyProjector(nn.Module):
         """Autograd path of run_pooled (torch ops on [N, <= 512] rows): -> (w, mean, logvar)."""
         n, in_features = pooled.shape
         if in_features != self.in_channels:
-            # reference quirk (:225-230): fresh nn.Linear on EVERY call, drawn from the CPU generator
-            self.fc1 = _fresh_linear(in_features, 256, pooled.device)
+            self.refresh_fc1(in_features, pooled.device)
         h = F.leaky_relu(F.linear(pooled, self.fc1.weight, self.fc1.bias), self.act.negative_slope)
         p = F.linear(h, self.fc2.weight, self.fc2.bias).view(n, self.num_ws, self.w_dim * 2)
         mean, logvar = torch.chunk(p, 2, dim=2)

@@ -17,7 +17,10 @@ Deviations, all explicit:
   * Without fp16 the reference runs its forward under ``torch.no_grad()`` (:668) and its loss.backward()
     then fails; this step always builds the graph (the reference's fp16 branch: autocast + GradScaler; here
     ``precision='bf16'`` on the modules, which needs no loss scaling).
-  * Multi-GPU: data parallel, one process per GPU, gradients averaged by distributed.allreduce_gradients.
+  * Multi-GPU: data parallel, one process per GPU, gradients averaged by distributed.allreduce_gradients.  The
+    fine projector's fc1, which the reference re-creates from the CPU generator on every call (:225-230), is
+    broadcast from rank 0 after each re-creation, so every rank runs -- and averages the gradients of -- the same
+    weights (or build the encoder with fix_fine_projector=True: no re-creation at all).
 """
 from __future__ import annotations
 
@@ -50,6 +53,22 @@ def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_
                          "weights are not available offline): pass percep=... or perceptual_weight=0")
     encoder = compressor.encoder
     optimizer.zero_grad()
+    world = sync_gradients if sync_gradients is not None else (
+        torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1)
+    projectors = (encoder.global_projector, encoder.medium_projector, encoder.fine_projector)
+    if world > 1:
+        for proj in projectors:
+            proj.fc1_hook = icd.broadcast_params
+    try:
+        return _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight,
+                           percep, second_encoder_pass, sync_gradients)
+    finally:
+        for proj in projectors:
+            proj.fc1_hook = None
+
+
+def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight, percep,
+                second_encoder_pass, sync_gradients):
     with torch.enable_grad():
         if second_encoder_pass:
             reconstructed, _ = compressor(images)

@@ -87,3 +87,26 @@ def test_out_of_range_and_corrupt_input_fail_loudly():
         cc.cabac_decode(blob, cc.ContextModel(n_symbols=256))
     with pytest.raises(ValueError):
         cc.cabac_decode(blob, cm, (1, 2, 9))
+
+
+def test_untrusted_header_cannot_force_a_huge_allocation():
+    """ADVICE r2 (decompression bomb): a ~256 KiB file must not make cabac_decode allocate b * num_ws * w_dim int32
+    codes far beyond what its payload can hold -- the total is capped, and each stream's size must be able to
+    hold its symbols (>= 5 bytes, <= 64 symbols per byte: the coder's probability floor allows ~45)."""
+    import struct
+    cm = cc.ContextModel(n_symbols=256)
+    b, num_ws, w_dim = 65536, 16, 1 << 20          # 2^24 symbols per stream, 2^40 in total
+    head = struct.pack("<4s5I", b"IC2R", 1, b, num_ws, w_dim, 256) + struct.pack(f"<{b}I", *([0] * b))
+    with pytest.raises(ValueError, match="implausible"):
+        cc.cabac_decode(head, cm)
+    b, num_ws, w_dim = 16, 16, 1 << 20              # within the total cap, but zero-length streams
+    head = struct.pack("<4s5I", b"IC2R", 1, b, num_ws, w_dim, 256) + struct.pack(f"<{b}I", *([0] * b))
+    with pytest.raises(ValueError, match="implausible"):
+        cc.cabac_decode(head, cm)
+    # 5-byte streams claiming 2^24 symbols each: more than 5 bytes can decode to
+    head = struct.pack("<4s5I", b"IC2R", 1, b, num_ws, w_dim, 256) + struct.pack(f"<{b}I", *([5] * b)) + bytes(5 * b)
+    with pytest.raises(ValueError, match="implausible"):
+        cc.cabac_decode(head, cm)
+    # the densest genuine stream (constant codes) is still accepted
+    codes = np.full((1, 16, 4096), 7, dtype=np.int32)
+    assert np.array_equal(cc.cabac_decode(cc.cabac_encode(codes, cm), cm), codes)

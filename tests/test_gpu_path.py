@@ -67,6 +67,20 @@ def test_modconv_prep_batched_equals_per_layer(cuda, gen256, dt):
         assert torch.equal(got[i][1], os_), (i, "oscale")
 
 
+def test_modconv_prep_per_layer_fallback(cuda, gen256):
+    """Layers wider than the batched prep's 512-long rows (channel_max > 512) take ic2_fc + ic2_modconv_prep: the
+    same coefficients (forced here on the 512-wide generator) to f32 rounding."""
+    syn = gen256.synthesis
+    n = 3
+    ws = (torch.randn(n, syn.num_ws, syn.w_dim, generator=torch.Generator().manual_seed(8)) * 1.5).to(cuda)
+    ldx = syn.num_ws * syn.w_dim
+    flat = ws.view(-1)
+    for i, L in enumerate(syn.layers()):
+        xs, os_ = L.scales(flat[(i + 1) * syn.w_dim:], ldx, n, torch.float32)
+        xu, ou = L.scales(flat[(i + 1) * syn.w_dim:], ldx, n, torch.float32, unbatched=True)
+        assert torch.allclose(xs, xu, rtol=1e-5, atol=1e-6) and torch.allclose(os_, ou, rtol=1e-5, atol=1e-6), i
+
+
 def test_synthesis_input_matches_oracle(cuda, gen256):
     sd = _sd_cpu(gen256)
     inp, _ = sg3.layer_table(256)
