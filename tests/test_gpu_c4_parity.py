@@ -1,0 +1,118 @@
+"""Parity of the benched mode on the C4 workload (BASELINE.json configs[3]): HVAE_VGG_Encoder(img_resolution=1024) on
+1024^2 input -> 8-bit uniform quantizer -> SG3-T-1024 synthesis (up-4 layers at 276 / 532 / 1044, the 2098^2
+lrelu grids, the 81 / 51 / 32-channel tail), in bench.py's default precisions (encoder split-bf16 'bf16x3',
+synthesis bf16), at a batch the CPU oracle can afford.
+
+Reference path: stylegan3_hvae_full.py:295-329 (compress -> decompress), metric hvae_training.py:368-395.
+The oracle means come from oracle/encoder.py (pinned to the reference's encoder by tests/golden/encoder_full.npz);
+the reference reconstruction is the fp32 path on the oracle's quantized latents, itself pinned to the CPU synthesis
+restatement at 1e-3 (test_gpu_path.py::test_synthesis_1024_fp32_within_1e3_of_oracle).
+Asserted as in test_gpu_c2_parity.py: index mismatches vs the oracle, synthesis-only and end-to-end SNR floors, the
+north-star PSNR delta at the README's 34 dB operating point, and a one-bf16-ulp-per-layer perturbation the floor
+catches.  Thresholds measured on MI355X are recorded in DESIGN.md (c).
+"""
+import numpy as np
+import pytest
+import torch
+
+import image_compression_2_amd as ic2
+from image_compression_2_amd import metrics as icm
+from oracle import encoder as oe
+
+pytestmark = pytest.mark.gpu
+
+B = 2
+ENC_TOL = 5e-5          # max |means_bench - means_oracle| (8-bit step 2/255 = 0.0078)
+IDX_FRAC = 1e-3         # fraction of the 8-bit indices that may differ (by one) from the oracle's
+HALF_STEP = 1e-4        # a differing index's oracle latent lies within this of a rounding boundary
+SNR_FLOOR_SYN = 36.0    # dB, bf16 SG3-T-1024 synthesis vs the fp32 reference on identical latents
+SNR_FLOOR_E2E = 36.0    # dB, benched encode + quantize + synthesis vs the reference reconstruction
+PSNR_TOL = 0.01         # dB at the 34 dB operating point (north star)
+
+
+def _snr_db(a, ref):
+    a, ref = a.double().cpu(), ref.double().cpu()
+    return 10 * np.log10((ref ** 2).sum().item() / max(((a - ref) ** 2).sum().item(), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def c4(cuda):
+    import bench
+    enc_prec, syn_prec = bench.PRECISIONS["bf16"]
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=1024).to(cuda).eval().requires_grad_(False)
+    x = torch.rand(B, 3, 1024, 1024, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+    with torch.no_grad():
+        torch.manual_seed(5)  # the fine projector re-draws fc1 from the CPU RNG (ref :225-230)
+        _, m_b, _ = enc(x.to(cuda))
+        fc1 = (enc.fine_projector.fc1.weight.detach().cpu(), enc.fine_projector.fc1.bias.detach().cpu())
+        sd = {k: v.detach().cpu() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
+        _, m_or, _ = oe.encoder_forward(sd, x, fine_fc1=fc1)
+        q_b = ic2.quantize_uniform(m_b, 8)
+        q_or = oe.quantize_uniform(m_or, 8)
+        G.set_precision("fp32")
+        ref = G.synthesis(q_or.to(cuda)).cpu()
+        G.set_precision(syn_prec)
+        img_e2e = G.synthesis(q_b).cpu()
+        img_syn = G.synthesis(q_or.to(cuda)).cpu()
+        G.set_precision("fp32")
+    return dict(G=G, m_b=m_b.cpu(), m_or=m_or, q_or=q_or, ref=ref, img_e2e=img_e2e, img_syn=img_syn,
+                syn_prec=syn_prec)
+
+
+def test_c4_bench_indices_vs_oracle(c4):
+    m, m_or = c4["m_b"], c4["m_or"]
+    err = (m - m_or).abs()
+    d = oe.uniform_indices(m, 8) - oe.uniform_indices(m_or, 8)
+    mism = d != 0
+    u = (m_or.double() + 1) * 0.5 * 255
+    dist = ((u - u.floor() - 0.5).abs() * 2 / 255)[mism]
+    frac = mism.float().mean().item()
+    print(f"[c4] encoder (bench mode, 1024^2) vs oracle: max|dm| = {err.max().item():.3e}, index mismatches "
+          f"{int(mism.sum())}/{mism.numel()} = {frac:.2e}, max half-step distance of a mismatch = "
+          f"{dist.max().item() if dist.numel() else 0.0:.3e}")
+    assert err.max().item() < ENC_TOL
+    assert d.abs().max().item() <= 1 and frac <= IDX_FRAC and (dist <= HALF_STEP).all()
+
+
+def test_c4_reconstruction_snr(c4):
+    syn, e2e = _snr_db(c4["img_syn"], c4["ref"]), _snr_db(c4["img_e2e"], c4["ref"])
+    print(f"[c4] {c4['syn_prec']} SG3-T-1024 synthesis-only SNR {syn:.2f} dB (uint8 PSNR "
+          f"{icm.psnr(c4['img_syn'], c4['ref']):.2f}); end-to-end SNR {e2e:.2f} dB")
+    assert syn > SNR_FLOOR_SYN and e2e > SNR_FLOOR_E2E
+
+
+@pytest.mark.parametrize("sigma,tol", [(0.039, PSNR_TOL), (0.01, None)])
+def test_c4_psnr_bar(c4, sigma, tol):
+    g = torch.Generator().manual_seed(78)
+    ref = c4["ref"]
+    target = ref + sigma * torch.randn(ref.shape, generator=g)
+    p_ref = icm.psnr(ref, target)
+    out = {k: icm.psnr(c4[k], target) - p_ref for k in ("img_syn", "img_e2e")}
+    print(f"[c4] sigma={sigma}: PSNR(reference) = {p_ref:.3f} dB; delta synthesis-only {out['img_syn']:+.4f} dB, "
+          f"end-to-end {out['img_e2e']:+.4f} dB")
+    if tol is not None:
+        assert abs(out["img_syn"]) < tol and abs(out["img_e2e"]) < tol
+
+
+def test_c4_snr_floor_detects_one_ulp_per_layer(c4):
+    """The floor is not vacuous at 1024^2 either: a 2^-8 (one bf16 ulp) error in every layer's filtered-lrelu gain
+    pushes the synthesis-only SNR below SNR_FLOOR_SYN."""
+    G = c4["G"]
+    layers = [L for L in G.synthesis.layers() if not L.is_torgb]
+    saved = [L.act_gain for L in layers]
+    try:
+        for L in layers:
+            L.act_gain = L.act_gain * (1 + 2 ** -8)
+        G.set_precision(c4["syn_prec"])
+        with torch.no_grad():
+            img = G.synthesis(c4["q_or"].to(next(G.parameters()).device)).cpu()
+    finally:
+        G.set_precision("fp32")
+        for L, g_ in zip(layers, saved):
+            L.act_gain = g_
+    snr = _snr_db(img, c4["ref"])
+    print(f"[c4] perturbed (gain, 2^-8 per layer): synthesis SNR {snr:.2f} dB")
+    assert snr < SNR_FLOOR_SYN
