@@ -53,10 +53,10 @@ def c4(cuda):
         q_b = ic2.quantize_uniform(m_b, 8)
         q_or = oe.quantize_uniform(m_or, 8)
         G.set_precision("fp32")
-        ref = G.synthesis(q_or.to(cuda)).cpu()
+        ref = G.synthesis(q_or.to(cuda))
         G.set_precision(syn_prec)
-        img_e2e = G.synthesis(q_b).cpu()
-        img_syn = G.synthesis(q_or.to(cuda)).cpu()
+        img_e2e = G.synthesis(q_b)
+        img_syn = G.synthesis(q_or.to(cuda))
         G.set_precision("fp32")
     return dict(G=G, m_b=m_b.cpu(), m_or=m_or, q_or=q_or, ref=ref, img_e2e=img_e2e, img_syn=img_syn,
                 syn_prec=syn_prec)
@@ -88,7 +88,7 @@ def test_c4_reconstruction_snr(c4):
 def test_c4_psnr_bar(c4, sigma, tol):
     g = torch.Generator().manual_seed(78)
     ref = c4["ref"]
-    target = ref + sigma * torch.randn(ref.shape, generator=g)
+    target = ref + (sigma * torch.randn(ref.shape, generator=g)).to(ref.device)
     p_ref = icm.psnr(ref, target)
     out = {k: icm.psnr(c4[k], target) - p_ref for k in ("img_syn", "img_e2e")}
     print(f"[c4] sigma={sigma}: PSNR(reference) = {p_ref:.3f} dB; delta synthesis-only {out['img_syn']:+.4f} dB, "
@@ -108,7 +108,7 @@ def test_c4_snr_floor_detects_one_ulp_per_layer(c4):
             L.act_gain = L.act_gain * (1 + 2 ** -8)
         G.set_precision(c4["syn_prec"])
         with torch.no_grad():
-            img = G.synthesis(c4["q_or"].to(next(G.parameters()).device)).cpu()
+            img = G.synthesis(c4["q_or"].to(next(G.parameters()).device))
     finally:
         G.set_precision("fp32")
         for L, g_ in zip(layers, saved):

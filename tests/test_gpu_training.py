@@ -310,8 +310,9 @@ def test_synthesis_refuses_weight_gradients(cuda, gen256_frozen):
     ws = torch.randn(1, 16, 512, device=cuda, requires_grad=True)
     G.synthesis.L3_52_512.weight.requires_grad_(True)
     try:
+        out = G.synthesis(ws)            # the inference forward runs (grad-mode inference keeps working) ...
         with pytest.raises(nv.AutogradUnsupported):
-            G.synthesis(ws)
+            out.sum().backward()         # ... and the backward refuses: weight gradients are not implemented
     finally:
         G.synthesis.L3_52_512.weight.requires_grad_(False)
 
