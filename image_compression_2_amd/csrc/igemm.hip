@@ -1421,6 +1421,17 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
   return buf;
 }
 
+// Images per launch: the buffer-descriptor kernels (8-phase, hg4) address < 2^31 bytes per operand, so a batch whose
+// input exceeds that runs in chunks of whole images (each chunk with its own launch plan) instead of falling back to
+// the generic tile (SG3-T-1024 / the 1024^2 encoder at batch 8: 1024^2 x 192 x 2 B = 403 MB per image).
+static int conv_chunk_n(int dtype, int n, int h, int w_, int cin_p) {
+  const int64_t per_img = (int64_t)h * w_ * cin_p * (dtype == IC2_F32 ? 4 : 2);
+  if ((int64_t)n * per_img < (int64_t)kOob || per_img >= (int64_t)kOob) return n;
+  const int64_t c = ((int64_t)kOob - 1) / per_img;
+  const int64_t chunks = ceil_div(n, c);
+  return (int)ceil_div(n, chunks);  // balanced chunks
+}
+
 }  // namespace ic2
 
 using namespace ic2;
@@ -1429,16 +1440,18 @@ extern "C" const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, i
                                      int cout_p, int cout_valid, int kh, int kw, int pad) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (n <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0) return "invalid";
-  const ConvChoice c = conv_choice(dtype, out_layout, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
-  return conv_choice_name(c, dtype, n, ho, wo, cin_p, cout_p);
+  const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
+  const ConvChoice c = conv_choice(dtype, out_layout, out_dtype, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  return conv_choice_name(c, dtype, nc, ho, wo, cin_p, cout_p);
 }
 
 extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
                                            int pad) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
-  const ConvChoice c = conv_choice(dtype, IC2_LAYOUT_NHWC, dtype, n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad);
-  return c.kind == CK_IGEMM && c.pl.splits > 1 ? (int64_t)c.pl.splits * n * ho * wo * cout_p * 4 : 0;
+  const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
+  const ConvChoice c = conv_choice(dtype, IC2_LAYOUT_NHWC, dtype, nc, h, w_, cin_p, cout_p, cout_p, kh, kw, pad);
+  return c.kind == CK_IGEMM && c.pl.splits > 1 ? (int64_t)c.pl.splits * nc * ho * wo * cout_p * 4 : 0;
 }
 
 extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
@@ -1460,6 +1473,22 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                 "conv_igemm: NCHW output needs f32 and 0 < cout_valid <= cout_p (layout %d)", out_layout);
   IC2_CHECK_ARG(((uintptr_t)oscale | (uintptr_t)bias | (uintptr_t)workspace) % 16 == 0,
                 "conv_igemm: oscale/bias/workspace must be 16-byte aligned");
+  const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
+  if (nc < n) {
+    const int64_t x_img = (int64_t)h * w_ * cin_p * (dtype == IC2_F32 ? 4 : 2);
+    const int64_t y_img = out_layout == IC2_LAYOUT_NCHW ? (int64_t)cout_valid * ho * wo * 4
+                                                        : (int64_t)ho * wo * cout_p * (out_dtype == IC2_F32 ? 4 : 2);
+    for (int n0 = 0; n0 < n; n0 += nc) {
+      const int nn = n - n0 < nc ? n - n0 : nc;
+      const int rc = ic2_conv_igemm_ws(reinterpret_cast<const char*>(x) + n0 * x_img, w,
+                                       reinterpret_cast<char*>(y) + n0 * y_img, dtype, out_dtype, nn, h, w_, cin_p,
+                                       cout_p, cout_valid, kh, kw, pad, ho, wo,
+                                       oscale ? oscale + (int64_t)n0 * cout_p : nullptr, bias, act, slope, act_gain,
+                                       clamp, out_mul, out_layout, workspace, ws_bytes, stream);
+      if (rc != IC2_OK) return rc;
+    }
+    return IC2_OK;
+  }
   const int64_t M = (int64_t)n * ho * wo;
   IC2_CHECK_ARG(M < (1LL << 30), "conv_igemm: too many output pixels");
   IgemmArgs a;

@@ -122,3 +122,27 @@ def test_every_default_plan_instance_matches_fp32(cuda, default_plan_instances):
         err = (got - ref).abs().max().item()
         print(f"[plan] {p}: n={n} {g['h']}x{g['w']} {g['cin_p']}->{g['cout_p']} max|err| {err:.2e}")
         assert err < tol, p
+
+
+def test_batch_chunking_past_2gib(cuda):
+    """A batch whose input exceeds the buffer descriptors' 2 GiB (the C4 encoder's split-bf16 block-0 conv2: 8 x 1024^2
+    x 192 bf16 = 3.2 GB) runs in chunks of whole images, each on the halo GEMM, and equals the per-image launches."""
+    n, h, cin_p, cout_p = 8, 1024, 192, 64
+    assert nv.conv_plan(nv.BF16, nv.F32, nv.NHWC, n, h, h, cin_p, cout_p, cout_p, 3, 3, 1).startswith("hg4_o64")
+    gen = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(n, h, h, cin_p, generator=gen, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(cout_p, 3, 3, cin_p, generator=gen, device=cuda) / (9 * cin_p) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(cout_p, generator=gen, device=cuda) * 0.1
+    y = torch.empty(n, h, h, cout_p, device=cuda)
+    st = nv.stream_of(x)
+    nv.conv_igemm(nv.ptr(x), nv.ptr(w), nv.ptr(y), nv.BF16, nv.F32, n, h, h, cin_p, cout_p, cout_p, 3, 3, 1, h, h, None,
+                  nv.ptr(bias), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, st, cuda)
+    y1 = torch.empty(1, h, h, cout_p, device=cuda)
+    for i in (0, 3, 7):
+        xi = x[i:i + 1].contiguous()
+        nv.conv_igemm(nv.ptr(xi), nv.ptr(w), nv.ptr(y1), nv.BF16, nv.F32, 1, h, h, cin_p, cout_p, cout_p, 3, 3, 1, h,
+                      h, None, nv.ptr(bias), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, st, cuda)
+        err = (y[i] - y1[0]).abs().max().item()
+        assert err < 1e-4 * (1 + y1.abs().max().item()), (i, err)
+    del x, y
+    torch.cuda.empty_cache()
