@@ -259,7 +259,9 @@ def torch_dtype(precision):
         return torch.float32
     if precision in ("bf16", torch.bfloat16):
         return torch.bfloat16
-    raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+    if precision in ("f16", "fp16", torch.float16):
+        return torch.float16
+    raise ValueError(f"precision must be 'fp32', 'bf16' or 'f16', got {precision!r}")
 
 
 ENCODER_PRECISIONS = ("fp32", "bf16", "bf16x3")
@@ -270,7 +272,7 @@ def encoder_dtype(precision):
     IC2_BF16X3): bf16 MFMA operands [hi | hi | lo] x [hi | lo | hi], f32 conv outputs, GroupNorm in f32."""
     if precision == "bf16x3":
         return torch.bfloat16, True
-    if precision in ENCODER_PRECISIONS:
+    if precision in ("fp32", "bf16"):
         return torch_dtype(precision), False
     raise ValueError(f"encoder precision must be one of {ENCODER_PRECISIONS}, got {precision!r}")
 

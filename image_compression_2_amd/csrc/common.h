@@ -59,6 +59,14 @@ template <> struct Elem<bf16_t> {
   __device__ static __forceinline__ void store(bf16_t* p, float v) { *p = f2bf(v); }
 };
 
+// f16 elements (the synthesis's f16 mode): stores saturate to the f16 range instead of overflowing to inf
+template <> struct Elem<_Float16> {
+  __device__ static __forceinline__ float load(const _Float16* p) { return (float)*p; }
+  __device__ static __forceinline__ void store(_Float16* p, float v) {
+    *p = (_Float16)__builtin_amdgcn_fmed3f(v, -65504.f, 65504.f);
+  }
+};
+
 template <typename T> __device__ __forceinline__ float ld(const T* p) { return Elem<T>::load(p); }
 template <typename T> __device__ __forceinline__ void st(T* p, float v) { Elem<T>::store(p, v); }
 

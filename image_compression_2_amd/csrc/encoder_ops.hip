@@ -507,6 +507,9 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, x, (bf16_t*)y, n, c, h * w,
                        c_p, scale);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<_Float16>, dim3(grid_1d(total)), dim3(256), 0, s, x, (_Float16*)y, n, c,
+                       h * w, c_p, scale);
   else if (dtype == IC2_BF16X3)
     hipLaunchKernelGGL(nchw_to_nhwc_x3_kernel, dim3(grid_1d(total)), dim3(256), 0, s, x, (bf16_t*)y, n, c, h * w, c_p,
                        scale);
@@ -672,6 +675,9 @@ extern "C" int ic2_nhwc_to_nchw(const void* x, int dtype, float* y, int n, int c
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, dim3(grid_1d(total)), dim3(256), 0, s, (const bf16_t*)x, y, n, c,
                        h * w, c_p);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<_Float16>, dim3(grid_1d(total)), dim3(256), 0, s, (const _Float16*)x, y, n,
+                       c, h * w, c_p);
   else
     IC2_CHECK_ARG(false, "nhwc_to_nchw: bad dtype");
   IC2_CHECK_LAUNCH("nhwc_to_nchw");

@@ -18,13 +18,14 @@ struct FlrArgs {
   int py0, px0;                 // leading padding
   int tiles_x, tiles_y, cblocks, nimg;
   int order;  // wide MFMA kernel: tile order, 0 = channel block fastest, 1 = x, y fastest (one plane per XCD run)
+  int out_f16;  // MFMA kernels: output f16 (saturated) instead of bf16 (the synthesis's f16 mode)
   float slope, lim;  // lrelu slope (<= 1) and clamp bound / gain (+inf = no clamp)
   float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
   float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
   float gd[12];  // flipped (unless flip_filter)
 };
 
-// NHWC or channel-blocked NHWC16 (strides in a), f16 (in_f16) or bf16 input, bf16 output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
+// NHWC or channel-blocked NHWC16 (strides in a), f16 (in_f16) or bf16 input, bf16 or f16 (a.out_f16) output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
 // bias (folded into the producer).  Sets tiles/cblocks itself.  Returns IC2_E_UNSUPPORTED when the
 // configuration has no MFMA instance.
 int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, int delta, int n, hipStream_t s);

@@ -349,8 +349,9 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
   static const bool use_mfma = knob("IC2_FLR_MFMA", 1) != 0;
   // f16 input (the synthesis conv epilogue's output) exists only for the MFMA formulation
   // (one polyphase phase for both axes: the instances take a single delta)
-  const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) && dtype_out == IC2_BF16 && b == nullptr &&
-                       dx == dy;
+  const bool mfma_ok = chlast && (dtype_in == IC2_BF16 || dtype_in == IC2_F16) &&
+                       (dtype_out == IC2_BF16 || dtype_out == IC2_F16) && b == nullptr && dx == dy;
+  a.out_f16 = dtype_out == IC2_F16;
   if ((use_mfma || dtype_in == IC2_F16) && mfma_ok) {
     for (int t = 0; t < 24; ++t) a.gu[t] = 0.f;
     for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;
@@ -365,12 +366,12 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
     }
   }
   if (in_blocked) {
-    set_error("%s: channel-blocked input needs the MFMA instance (f16/bf16 in, bf16 out, no bias, up 2/4 with 6*up "
+    set_error("%s: channel-blocked input needs the MFMA instance (f16/bf16 in, bf16/f16 out, no bias, up 2/4 with 6*up "
               "taps, down 2 / 12 taps)", name);
     return IC2_E_UNSUPPORTED;
   }
   if (dtype_in == IC2_F16) {
-    set_error("%s: f16 input needs the MFMA instance (NHWC, bf16 out, no bias, up 2/4 with 6*up taps, down 2 / 12 taps)",
+    set_error("%s: f16 input needs the MFMA instance (NHWC, bf16/f16 out, no bias, up 2/4 with 6*up taps, down 2 / 12 taps)",
               name);
     return IC2_E_UNSUPPORTED;
   }

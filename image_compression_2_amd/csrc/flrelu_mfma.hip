@@ -102,6 +102,16 @@ __device__ __forceinline__ uint32_t fm_bf2_to_h2(uint32_t v) {
   return fm_h2u(lo, hi);
 }
 
+// the output quad (bf16, or f16 saturated in the synthesis's f16 mode)
+__device__ __forceinline__ uint2 fm_out4(bool f16, float a, float b, float c, float d) {
+  if (f16) {
+    const float lo = -65504.f, hi = 65504.f;
+    return fm_pack4(__builtin_amdgcn_fmed3f(a, lo, hi), __builtin_amdgcn_fmed3f(b, lo, hi),
+                    __builtin_amdgcn_fmed3f(c, lo, hi), __builtin_amdgcn_fmed3f(d, lo, hi));
+  }
+  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+
 // lrelu + clamp on a pair in 5 instructions (gain folded into the horizontal down taps):
 // for 0 <= slope <= 1, med3(v, slope*v, lim) is lrelu(v) clamped from above wherever |slope*v| <= lim, and
 // the outer med3 finishes the clamp for the rest (no fmaxf: it would cost a canonicalizing max per value)
@@ -454,8 +464,7 @@ __global__ void __launch_bounds__(64 * NW) flrelu_mfma_kernel(FlrArgs a, int nti
     for (int i = 0; i < RR; ++i) {
       const int gx = ox0 + wave + NW * i;
       if (gy < a.out_h && gx < a.out_w) {
-        const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
-                                   (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
+        const uint2 v = fm_out4(a.out_f16, acc[i][0] * ps[0], acc[i][1] * ps[1], acc[i][2] * ps[2], acc[i][3] * ps[3]);
         *reinterpret_cast<uint2*>(yout + (((int64_t)n * a.out_h + gy) * a.out_w + gx) * a.c_p + c0 + 4 * g) = v;
       }
     }
@@ -781,8 +790,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
         off = (gy < a.out_h && gx < a.out_w)
                   ? (uint32_t)((((c0 >> 4) * a.out_h + gy) * a.out_w + gx) * 32 + 8 * g) - (uint32_t)(c0 * 2)
                   : FM_OOB;
-      const uint2 v = make_uint2((uint32_t)f2bf(acc[i][0] * ps[0]) | ((uint32_t)f2bf(acc[i][1] * ps[1]) << 16),
-                                 (uint32_t)f2bf(acc[i][2] * ps[2]) | ((uint32_t)f2bf(acc[i][3] * ps[3]) << 16));
+      const uint2 v = fm_out4(a.out_f16, acc[i][0] * ps[0], acc[i][1] * ps[1], acc[i][2] * ps[2], acc[i][3] * ps[3]);
       if constexpr (!(ABL & 8))
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, off, 0, 0);
     }

@@ -28,7 +28,20 @@
 namespace ic2 {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// The 2-byte operand MFMA: bf16 (v_mfma_f32_16x16x32_bf16) or f16 (v_mfma_f32_16x16x32_f16, the same rate on gfx950).
+// Fragments travel as raw 16-B bf16x8 registers either way (LDS-DMA / ds_read move bits), reinterpreted here.
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// 2-byte activation / weight dtypes (bf16 or f16): the same kernels, a different MFMA
+__host__ __device__ inline bool is16(int dtype) { return dtype == IC2_BF16 || dtype == IC2_F16; }
 
 struct IgemmArgs {
   const void* x;
@@ -205,7 +218,7 @@ __device__ __forceinline__ void tile_coords(int logical, int tiles_o, int tiles_
   p_tile = gi * group + (rem - o_tile * gsz);
 }
 
-template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
+template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE, bool F16 = false>
 __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
   using C = IgCfg<BF16, BO, BP, WGO, WGP, NSTAGE>;
   constexpr int EPC = C::EPC, ESZ = C::ESZ, I = C::I, J = C::J, NIW = C::NIW, NIX = C::NIX;
@@ -344,7 +357,7 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
       for (int i = 0; i < I; ++i)
 #pragma unroll
         for (int j = 0; j < J; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma32<F16>(af[i], bfr[j], acc[i][j]);
     } else {
       IC2_IG_ISSUE((q + NSTAGE - 1) % NSTAGE);
       __builtin_amdgcn_sched_barrier(0);
@@ -428,7 +441,7 @@ __device__ __forceinline__ int g8_off(int row, int chunk) { return row * 128 + (
 __device__ __forceinline__ int g8_arow(int qm, int g, int l) { return (g >> 3) * 128 + qm * 64 + (g & 7) * 8 + l; }
 __device__ __forceinline__ int g8_brow(int qn, int g, int l) { return (g >> 2) * 64 + qn * 32 + (g & 3) * 8 + l; }
 
-template <int OG>
+template <int OG, bool F16 = false>
 __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   using G = G8<OG>;
   constexpr int NA = G::NA, NB = G::NB;
@@ -591,7 +604,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   if ((qm_) == 0 ? live0 : live1) {                                                                          \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)             \
         _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + i][(qn_) * 2 + j] =                    \
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[(qm_) * 4 + i][(qn_) * 2 + j], 0, 0, 0); \
+            mfma32<F16>(af[i][s], bfr[j][s], acc[(qm_) * 4 + i][(qn_) * 2 + j]);                                   \
   }                                                                                                          \
   __builtin_amdgcn_s_setprio(0);                                                                             \
   __builtin_amdgcn_sched_barrier(0);                                                                         \
@@ -657,23 +670,27 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 // one non-template kernel per instance (a __global__ template's host stub is not emitted here)
 __global__ void __launch_bounds__(512, 1) igemm8_og2_kernel(IgemmArgs a) { igemm8_body<2>(a); }
 __global__ void __launch_bounds__(512, 1) igemm8_og1_kernel(IgemmArgs a) { igemm8_body<1>(a); }
+__global__ void __launch_bounds__(512, 1) igemm8_og2_f16_kernel(IgemmArgs a) { igemm8_body<2, true>(a); }
+__global__ void __launch_bounds__(512, 1) igemm8_og1_f16_kernel(IgemmArgs a) { igemm8_body<1, true>(a); }
 
-template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
+template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE, bool F16 = false>
 static void launch_igemm(IgemmArgs a, int splits, hipStream_t s) {
   a.tiles_o = (a.cout_p + BO - 1) / BO;
   a.nblocks = (int)(ceil_div(a.M, BP) * a.tiles_o);
-  hipLaunchKernelGGL((igemm_kernel<BF16, BO, BP, WGO, WGP, NSTAGE>), dim3(a.nblocks, splits), dim3(64 * WGO * WGP), 0,
-                     s, a);
+  hipLaunchKernelGGL((igemm_kernel<BF16, BO, BP, WGO, WGP, NSTAGE, F16>), dim3(a.nblocks, splits),
+                     dim3(64 * WGO * WGP), 0, s, a);
 }
 
-template <int OG>
+template <int OG, bool F16 = false>
 static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1) {
   a.o_base = o_base;
   a.tiles_o = ((o_end < 0 ? a.cout_p : o_end) - o_base + G8<OG>::BO - 1) / G8<OG>::BO;
   a.nq = a.K / 64;
   a.nblocks = (int)(ceil_div(a.M, G8<OG>::BP) * a.tiles_o);
-  if constexpr (OG == 2) hipLaunchKernelGGL(igemm8_og2_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(igemm8_og1_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+  if constexpr (OG == 2)
+    hipLaunchKernelGGL(F16 ? igemm8_og2_f16_kernel : igemm8_og2_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(F16 ? igemm8_og1_f16_kernel : igemm8_og1_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -712,7 +729,7 @@ __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((
 // HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
 // past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
 // chain, ~60 SALU per step) and a wait count that depends only on the tap
-template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false>
+template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = H4<I, J, WGO, WGP, TW, NS, HB>;
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
@@ -838,7 +855,7 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
 #pragma unroll
       for (int i = 0; i < I; ++i)
 #pragma unroll
-        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < J; ++j) acc[i][j] = mfma32<F16>(af[i], bfr[j], acc[i][j]);
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -884,11 +901,19 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
   __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
                                                                                           int ty) {            \
     hg4_body<I, J, WGO, WGP, TW, NS>(a, tx, ty);                                                                 \
+  }                                                                                                              \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name##_f16(IgemmArgs a,     \
+                                                                                                int tx, int ty) { \
+    hg4_body<I, J, WGO, WGP, TW, NS, false, true>(a, tx, ty);                                                    \
   }
 #define IC2_HG4_KERNEL_HB(name, I, J, WGO, WGP, TW, NS)                                                          \
   __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
                                                                                           int ty) {            \
     hg4_body<I, J, WGO, WGP, TW, NS, true>(a, tx, ty);                                                           \
+  }                                                                                                              \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name##_f16(IgemmArgs a,     \
+                                                                                                int tx, int ty) { \
+    hg4_body<I, J, WGO, WGP, TW, NS, true, true>(a, tx, ty);                                                     \
   }
 // the launch plan's instances: halo-burst (HB) kernels for 32-wide pixel tiles, 4-slab rings for 16-wide ones
 IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)  // 128 o x (16 x 16) px
@@ -933,16 +958,16 @@ static void launch_hg4(IgemmArgs a, hipStream_t s, void (*kern)(IgemmArgs, int, 
 
 // the halo burst on 32-wide tiles (s276a +2.6 %, s276b +3 %, SG3-T-1024 L11 +7 % over spreading the halo DMAs over
 // the first taps, profiles/r2f_hg4_hb.txt); a 4-slab weight ring (+0.5-1 % over 3, profiles/r2e_hg4_sweep.txt)
-static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
+static void hg4_dispatch(const IgemmArgs& a, hipStream_t s, bool f16) {
   const H4Plan p = h4_plan(a.n, a.ho, a.wo, a.cout_p);
   if (p.tw32) {
-    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, hg4_o192_w32_hb_kernel);
-    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_hb_kernel);
-    else launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_hb_kernel);
+    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, f16 ? hg4_o192_w32_hb_kernel_f16 : hg4_o192_w32_hb_kernel);
+    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, f16 ? hg4_o128_w32_hb_kernel_f16 : hg4_o128_w32_hb_kernel);
+    else launch_hg4<4, 4, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_hb_kernel_f16 : hg4_o64_w32_hb_kernel);
   } else {
-    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 16>(a, s, hg4_o192_w16_s4_kernel);
-    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 16>(a, s, hg4_o128_w16_s4_kernel);
-    else launch_hg4<4, 4, 1, 4, 16>(a, s, hg4_o64_w16_s4_kernel);
+    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 16>(a, s, f16 ? hg4_o192_w16_s4_kernel_f16 : hg4_o192_w16_s4_kernel);
+    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 16>(a, s, f16 ? hg4_o128_w16_s4_kernel_f16 : hg4_o128_w16_s4_kernel);
+    else launch_hg4<4, 4, 1, 4, 16>(a, s, f16 ? hg4_o64_w16_s4_kernel_f16 : hg4_o64_w16_s4_kernel);
   }
 }
 
@@ -950,7 +975,7 @@ static void hg4_dispatch(const IgemmArgs& a, hipStream_t s) {
 // out, >= 93 % pixel-tile utilisation (tools/sweep_igemm.py, profiles/r2e_hg4_sweep.txt).  Knob IC2_HG4 (IC2_DEV=1):
 // 0 disables it, 2 forces it wherever legal (the tests' forced-instance runs).
 static bool hg4_legal(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems) {
-  return dtype == IC2_BF16 && kh == 3 && kw == 3 && cin_p % 32 == 0 && cout_p % 64 == 0 &&
+  return is16(dtype) && kh == 3 && kw == 3 && cin_p % 32 == 0 && cout_p % 64 == 0 &&
          x_elems * 2 < (int64_t)kOob && (int64_t)cout_p * 9 * cin_p * 2 < (int64_t)kOob;
 }
 static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems, int n, int ho, int wo) {
@@ -982,7 +1007,7 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
   static const bool splitk = knob("IC2_IGEMM_SPLITK", 1) != 0;
   const int64_t K = (int64_t)kh * kw * cin_p;
   int tile = 0;
-  if (dtype == IC2_BF16) {
+  if (is16(dtype)) {
     // o-tile: the widest of {256, 128, 64, 32} that divides cout_p (no padded MFMA rows), 256-pixel
     // tiles while the grid keeps >= 2 workgroups per CU, else the 128 x 128 tile
     const bool big_m = ceil_div(M, 256) * ((cout_p + 255) / 256) >= 512;
@@ -1060,9 +1085,10 @@ struct HcCfg {
   static constexpr int PER_T = (NPIECE + 511) / 512;
 };
 
-template <int CINP, int COUTP, int TH, bool GN>
+template <int CINP, int COUTP, int TH, bool GN, bool F16 = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(CINP == 32 ? 4 : 1)))
 hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
+  static_assert(!(F16 && GN), "the fused GroupNorm statistics are an encoder (bf16) feature");
   using C = HcCfg<CINP, COUTP, TH>;
   __shared__ __attribute__((aligned(16))) char lds[C::HALO_B + C::W_B];
   char* const halo = lds;
@@ -1159,7 +1185,7 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
         for (int i = 0; i < C::OB; ++i)
 #pragma unroll
           for (int j = 0; j < C::JB; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma32<F16>(af[i], bfr[j], acc[i][j]);
       }
     }
 
@@ -1257,7 +1283,7 @@ hconv_kernel(IgemmArgs a, int tiles_x, int tiles_y, int ntiles) {
   }
 }
 
-template <int CINP, int COUTP, bool GN = false>
+template <int CINP, int COUTP, bool GN = false, bool F16 = false>
 static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
   constexpr int TH = CINP > 64 ? 4 : 8;  // 96 channels: 4-row tiles keep halo + weight within 160 KB of LDS
   const int tiles_x = (int)ceil_div(a.wo, 32), tiles_y = (int)ceil_div(a.ho, TH);
@@ -1267,19 +1293,19 @@ static void launch_hconv(const IgemmArgs& a, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hconv_kernel<CINP, COUTP, TH, GN>, 512, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hconv_kernel<CINP, COUTP, TH, GN, F16>, 512, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL((hconv_kernel<CINP, COUTP, TH, GN>), dim3((unsigned)grid), dim3(512), 0, s, a, tiles_x, tiles_y,
-                     ntiles);
+  hipLaunchKernelGGL((hconv_kernel<CINP, COUTP, TH, GN, F16>), dim3((unsigned)grid), dim3(512), 0, s, a, tiles_x,
+                     tiles_y, ntiles);
 }
 
 // the halo kernel for bf16 3x3 convs with cin_p in {32, 64, 96}, cout_p in {32, 64} and >= 64K output
 // pixels; knob IC2_HCONV=0 keeps them on the implicit GEMM
 static bool hconv_eligible(int dtype, int64_t M, int cin_p, int cout_p, int kh, int kw) {
   static const bool on = knob("IC2_HCONV", 1) != 0;
-  return on && dtype == IC2_BF16 && kh == 3 && kw == 3 && (cin_p == 32 || cin_p == 64 || cin_p == 96) &&
+  return on && is16(dtype) && kh == 3 && kw == 3 && (cin_p == 32 || cin_p == 64 || cin_p == 96) &&
          (cout_p == 32 || cout_p == 64) && M >= 65536;
 }
 
@@ -1288,7 +1314,14 @@ static bool hconv_eligible(int dtype, int64_t M, int cin_p, int cout_p, int kh, 
 // VALU dot product instead of a 32-row MFMA tile that is 29/32 padding.  L = cin_p/16 lanes per pixel,
 // 16 channels (2 x 16 B) each, a fixed xor-shuffle tree over the L lanes, then the igemm epilogue math
 // (oscale, bias, activation / clamp, out_mul) on the group's first lane.
-template <int L, int CV>
+// 2-byte element -> f32 (bf16: the high half; f16: a conversion)
+template <bool F16>
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+  else return __uint_as_float(bits16 << 16);
+}
+
+template <int L, int CV, bool F16 = false>
 __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
   const int tid = blockIdx.x * 256 + threadIdx.x;
   const int sub = threadIdx.x & (L - 1);
@@ -1298,7 +1331,7 @@ __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
 #pragma unroll
   for (int o = 0; o < CV; ++o)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) wv[o][k] = __uint_as_float((uint32_t)wg[(int64_t)o * a.cin_p + sub * 16 + k] << 16);
+    for (int k = 0; k < 16; ++k) wv[o][k] = h2f<F16>(wg[(int64_t)o * a.cin_p + sub * 16 + k]);
   float bi[CV];
 #pragma unroll
   for (int o = 0; o < CV; ++o) bi[o] = a.bias ? a.bias[o] : 0.f;
@@ -1314,7 +1347,7 @@ __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
     for (int o = 0; o < CV; ++o) acc[o] = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float lo = __uint_as_float(w32[k] << 16), hi = __uint_as_float(w32[k] & 0xffff0000u);
+      const float lo = h2f<F16>(w32[k] & 0xffffu), hi = h2f<F16>(w32[k] >> 16);
 #pragma unroll
       for (int o = 0; o < CV; ++o) acc[o] = fmaf(wv[o][2 * k + 1], hi, fmaf(wv[o][2 * k], lo, acc[o]));
     }
@@ -1339,17 +1372,48 @@ __global__ void __launch_bounds__(256) torgb_kernel(IgemmArgs a) {
 static bool torgb_eligible(int dtype, int cin_p, int cout_valid, int kh, int kw, int pad, int out_layout,
                            int out_dtype) {
   static const bool on = knob("IC2_TORGB", 1) != 0;
-  return on && dtype == IC2_BF16 && kh == 1 && kw == 1 && pad == 0 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
+  return on && is16(dtype) && kh == 1 && kw == 1 && pad == 0 && cout_valid <= 4 && out_layout == IC2_LAYOUT_NCHW &&
          out_dtype == IC2_F32 && (cin_p == 32 || cin_p == 64 || cin_p == 128);
 }
 
+template <bool F16>
 static void launch_torgb(const IgemmArgs& a, hipStream_t s) {
   const int L = a.cin_p / 16;
   const int64_t need = ceil_div((int64_t)a.M * L, 256);
   const unsigned grid = (unsigned)(need < 8192 ? need : 8192);
-  if (L == 2) hipLaunchKernelGGL((torgb_kernel<2, 4>), dim3(grid), dim3(256), 0, s, a);
-  else if (L == 4) hipLaunchKernelGGL((torgb_kernel<4, 4>), dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((torgb_kernel<8, 4>), dim3(grid), dim3(256), 0, s, a);
+  if (L == 2) hipLaunchKernelGGL((torgb_kernel<2, 4, F16>), dim3(grid), dim3(256), 0, s, a);
+  else if (L == 4) hipLaunchKernelGGL((torgb_kernel<4, 4, F16>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((torgb_kernel<8, 4, F16>), dim3(grid), dim3(256), 0, s, a);
+}
+
+// the 2-byte (bf16 / f16) implicit-GEMM tiles and the halo conv configurations, by operand type
+template <bool F16>
+static void launch_igemm16(const IgemmArgs& a, hipStream_t s, const IgPlan& pl, bool split384, int cout_p) {
+  switch (pl.tile) {
+    case 6: launch_g8<2, F16>(a, s); break;
+    case 7:
+      if (split384) {
+        launch_g8<2, F16>(a, s, 0, cout_p - 128);
+        launch_g8<1, F16>(a, s, cout_p - 128, cout_p);
+      } else {
+        launch_g8<1, F16>(a, s);
+      }
+      break;
+    case 1: launch_igemm<true, 256, 256, 2, 4, 4, F16>(a, pl.splits, s); break;
+    case 2: launch_igemm<true, 32, 256, 1, 4, 4, F16>(a, pl.splits, s); break;
+    case 3: launch_igemm<true, 128, 256, 2, 4, 4, F16>(a, pl.splits, s); break;
+    case 5: launch_igemm<true, 64, 256, 1, 4, 4, F16>(a, pl.splits, s); break;
+    default: launch_igemm<true, 128, 128, 2, 2, 4, F16>(a, pl.splits, s); break;
+  }
+}
+template <bool F16>
+static void launch_hconv_cfg(const IgemmArgs& a, hipStream_t s, int cin_p, int cout_p) {
+  if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, false, F16>(a, s);
+  else if (cin_p == 32) launch_hconv<32, 64, false, F16>(a, s);
+  else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32, false, F16>(a, s);
+  else if (cin_p == 64) launch_hconv<64, 64, false, F16>(a, s);
+  else if (cout_p == 32) launch_hconv<96, 32, false, F16>(a, s);
+  else launch_hconv<96, 64, false, F16>(a, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1392,7 +1456,7 @@ static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, i
   // 128 channels, the 128 x 512 tile on those (both read the same input panel); knob IC2_IGEMM_SPLIT=0 keeps one
   // 128 x 512 launch
   static const bool split = knob("IC2_IGEMM_SPLIT", 1) != 0;
-  c.split384 = dtype == IC2_BF16 && c.pl.tile == 7 && split && cout_p % 256 == 128 && cout_p > 128 &&
+  c.split384 = is16(dtype) && c.pl.tile == 7 && split && cout_p % 256 == 128 && cout_p > 128 &&
                ceil_div(M, 256) >= 240;
   return c;
 }
@@ -1411,7 +1475,7 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
     }
     default: break;
   }
-  if (dtype != IC2_BF16) {
+  if (dtype == IC2_F32) {
     snprintf(buf, sizeof(buf), "igemm_f32_128x128%s", c.pl.splits > 1 ? "_splitk" : "");
     return buf;
   }
@@ -1442,7 +1506,11 @@ extern "C" const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, i
   if (n <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0) return "invalid";
   const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
   const ConvChoice c = conv_choice(dtype, out_layout, out_dtype, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
-  return conv_choice_name(c, dtype, nc, ho, wo, cin_p, cout_p);
+  const char* name = conv_choice_name(c, dtype, nc, ho, wo, cin_p, cout_p);
+  if (dtype != IC2_F16) return name;
+  static thread_local char f16_name[80];  // the f16-operand instance of the same kernel
+  snprintf(f16_name, sizeof(f16_name), "%s_f16", name);
+  return f16_name;
 }
 
 extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
@@ -1460,7 +1528,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                                  float clamp, float out_mul, int out_layout, void* workspace, int64_t ws_bytes,
                                  void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
-  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_igemm: bad dtype %d", dtype);
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16, "conv_igemm: bad dtype %d", dtype);
   IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
                 "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
@@ -1514,34 +1582,19 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   IgPlan& pl = c.pl;
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   switch (c.kind) {
-    case CK_TORGB: launch_torgb(a, s); break;
-    case CK_HG4: hg4_dispatch(a, s); break;
+    case CK_TORGB:
+      if (dtype == IC2_F16) launch_torgb<true>(a, s);
+      else launch_torgb<false>(a, s);
+      break;
+    case CK_HG4: hg4_dispatch(a, s, dtype == IC2_F16); break;
     case CK_HCONV:
-      if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32>(a, s);
-      else if (cin_p == 32) launch_hconv<32, 64>(a, s);
-      else if (cin_p == 64 && cout_p == 32) launch_hconv<64, 32>(a, s);
-      else if (cin_p == 64) launch_hconv<64, 64>(a, s);
-      else if (cout_p == 32) launch_hconv<96, 32>(a, s);
-      else launch_hconv<96, 64>(a, s);
+      if (dtype == IC2_F16) launch_hconv_cfg<true>(a, s, cin_p, cout_p);
+      else launch_hconv_cfg<false>(a, s, cin_p, cout_p);
       break;
     case CK_IGEMM:
-      if (dtype != IC2_BF16) launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
-      else switch (pl.tile) {
-        case 6: launch_g8<2>(a, s); break;
-        case 7:
-          if (c.split384) {
-            launch_g8<2>(a, s, 0, cout_p - 128);
-            launch_g8<1>(a, s, cout_p - 128, cout_p);
-          } else {
-            launch_g8<1>(a, s);
-          }
-          break;
-        case 1: launch_igemm<true, 256, 256, 2, 4, 4>(a, pl.splits, s); break;
-        case 2: launch_igemm<true, 32, 256, 1, 4, 4>(a, pl.splits, s); break;
-        case 3: launch_igemm<true, 128, 256, 2, 4, 4>(a, pl.splits, s); break;
-        case 5: launch_igemm<true, 64, 256, 1, 4, 4>(a, pl.splits, s); break;
-        default: launch_igemm<true, 128, 128, 2, 2, 4>(a, pl.splits, s); break;
-      }
+      if (dtype == IC2_F32) launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
+      else if (dtype == IC2_F16) launch_igemm16<true>(a, s, pl, c.split384, cout_p);
+      else launch_igemm16<false>(a, s, pl, c.split384, cout_p);
       if (pl.splits > 1) {
         const int64_t total = M * (cout_p / 4);
         const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);

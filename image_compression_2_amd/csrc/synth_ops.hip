@@ -506,6 +506,9 @@ extern "C" int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p, cin_p,
                        prenorm, scale, (bf16_t*)w_out, wsq_out);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(pack_weight_kernel<_Float16>, dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p, cin_p,
+                       prenorm, scale, (_Float16*)w_out, wsq_out);
   else if (dtype == IC2_BF16X3)
     hipLaunchKernelGGL((pack_weight_kernel<bf16_t, true>), dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p,
                        cin_p, prenorm, scale, (bf16_t*)w_out, wsq_out);
@@ -578,6 +581,9 @@ extern "C" int ic2_synth_input_features(const float* t, const float* freqs, cons
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(synth_input_kernel<bf16_t>, dim3((unsigned)(n * size)), dim3(256), 0, s, t, freqs, phases, transform,
                        n, c, c_p, size, sampling_rate, bandwidth, (bf16_t*)x_out);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(synth_input_kernel<_Float16>, dim3((unsigned)(n * size)), dim3(256), 0, s, t, freqs, phases,
+                       transform, n, c, c_p, size, sampling_rate, bandwidth, (_Float16*)x_out);
   else
     IC2_CHECK_ARG(false, "synth_input_features: bad dtype %d", dtype);
   IC2_CHECK_LAUNCH("synth_input_features");

@@ -14,7 +14,9 @@ seeded parameter construction order, and a forward that runs entirely in libic2o
 
 ``precision='bf16'`` stores activations and weights in bf16 (fp32 accumulate; the conv output that feeds
 the filtered lrelu is f16, whose FIR runs on MFMA with f16 operands and fp32 accumulation);
-``precision='fp32'`` (default) is the parity mode (exact-fp32 MFMA).
+``precision='f16'`` is the same pipeline with f16 activations and weights throughout (11-bit significands: about
+20 dB more synthesis SNR than bf16 at the same MFMA rate; outputs saturate at +-65504, far above conv_clamp);
+inference only (the autograd path trains in bf16).  ``precision='fp32'`` (default) is the parity mode (exact-fp32 MFMA).
 
 With grad mode on and ``ws`` requiring grad (the reference's encoder training backpropagates through the
 frozen generator, :669-696) ``SynthesisNetwork.forward`` takes the autograd path ``forward_train``: the same
@@ -383,10 +385,10 @@ class SynthesisLayer(torch.nn.Module):
                           nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW,
                           stream, x.device)
             return out
-        # bf16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16, in
+        # bf16 / f16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16, in
         # the channel-blocked layout [n][cout_p/16][conv][conv][16] the fused kernel's 16-channel tiles read as
         # contiguous rows (IC2_FLR_BLOCKED=0: plain NHWC)
-        ydt = torch.float16 if dt == torch.bfloat16 else dt
+        ydt = torch.float16 if dt in (torch.bfloat16, torch.float16) else dt
         blocked = ydt == torch.float16 and _FLR_BLOCKED
         if blocked:
             y = torch.empty([n, self.cout_p // 16, conv, conv, 16], dtype=ydt, device=x.device)
@@ -585,7 +587,8 @@ class SynthesisNetwork(torch.nn.Module):
         assert ws.ndim == 3 and ws.shape[1] == self.num_ws and ws.shape[2] == self.w_dim, ws.shape
         dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
         if _train_mode(self, ws):
-            return self.forward_train(ws, dt)
+            # 'f16' is an inference precision: the autograd path trains in bf16 (as the encoder's 'bf16x3')
+            return self.forward_train(ws, torch.bfloat16 if dt == torch.float16 else dt)
         ws_in = ws
         ws = ws.to(torch.float32).contiguous()
         nv.require_gpu(ws)

@@ -1,10 +1,10 @@
 """The default launch plan picks only instances that a parity check here has run.
 
-The benched workloads (bench.py C2 / C2g / C4, --precision bf16 and bf16-all) are run once with bench.CallTimer
+The benched workloads (bench.py C2 / C2g / C4, --precision bf16, bf16-all and f16) are run once with bench.CallTimer
 recording every conv call; ic2_conv_plan (the dispatcher's own plan function) names the kernel instance of each.
 For every distinct instance one of its own geometries (the batch reduced while the plan keeps the instance) is run
 under the default plan and compared with the library's exact-fp32 MFMA conv (v_mfma_f32_16x16x4_f32, pinned to fp64
-by test_gpu_kernels.py::test_conv_igemm[float32]) on the same bf16 operands: the two differ only in f32 summation
+by test_gpu_kernels.py::test_conv_igemm[float32]) on the same bf16 (f16) operands: the two differ only in f32 summation
 order.  Reference: the convs of HVAE_VGG_Encoder (stylegan3_hvae_full.py:62,175-176) and SG3 modulated_conv2d.
 """
 import pytest
@@ -17,11 +17,11 @@ from image_compression_2_amd import _native as nv
 pytestmark = pytest.mark.gpu
 
 
-def _record(cuda, res, gen_res, batch, enc_prec):
+def _record(cuda, res, gen_res, batch, enc_prec, gen_prec="bf16"):
     torch.manual_seed(0)
     enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
     torch.manual_seed(1)
-    G = ic2.Generator(img_resolution=gen_res, precision="bf16").to(cuda).eval().requires_grad_(False)
+    G = ic2.Generator(img_resolution=gen_res, precision=gen_prec).to(cuda).eval().requires_grad_(False)
     comp = ic2.StyleGAN3Compressor(enc, G)
     x = torch.rand(batch, 3, res, res, generator=torch.Generator().manual_seed(3)).to(cuda) * 2 - 1
     timer = bench.CallTimer(nv, bench.CONV_ENTRIES)
@@ -57,10 +57,10 @@ def _plan(g, n=None):
 def default_plan_instances(cuda):
     inst = {}
     for res, gen_res, batch in ((256, 256, 32), (1024, 1024, 8)):
-        for enc_prec in ("bf16x3", "bf16"):
+        for enc_prec, gen_prec in (("bf16x3", "bf16"), ("bf16", "bf16"), ("bf16x3", "f16")):
             if res == 1024 and enc_prec == "bf16":
                 continue
-            for name, a in _record(cuda, res, gen_res, batch, enc_prec):
+            for name, a in _record(cuda, res, gen_res, batch, enc_prec, gen_prec):
                 g = _geometry(name, a)
                 if g is None:
                     continue
@@ -75,19 +75,21 @@ def test_default_plan_instances_listed(default_plan_instances):
     names = sorted(default_plan_instances)
     print("[plan] instances on the benched workloads:", names)
     assert "igemm8_og2" in names and any(n.startswith("hg4_") for n in names)
+    assert "igemm8_og2_f16" in names and "torgb_f16" in names  # the synthesis's f16 mode
 
 
 def _run_conv(g, n, cuda, dt_in):
     gen = torch.Generator().manual_seed(n * 7 + g["cin_p"])
     ho, wo = g["h"] + 2 * g["pad"] - g["kh"] + 1, g["w"] + 2 * g["pad"] - g["kw"] + 1
-    x = (torch.randn(n, g["h"], g["w"], g["cin_p"], generator=gen)).to(torch.bfloat16)
+    op = torch.float16 if dt_in == nv.F16 else torch.bfloat16
+    x = (torch.randn(n, g["h"], g["w"], g["cin_p"], generator=gen)).to(op)
     w = (torch.randn(g["cout_p"], g["kh"], g["kw"], g["cin_p"], generator=gen) /
-         (g["kh"] * g["kw"] * g["cin_p"]) ** 0.5).to(torch.bfloat16)
+         (g["kh"] * g["kw"] * g["cin_p"]) ** 0.5).to(op)
     w[g["cv"]:] = 0
     bias = torch.randn(g["cout_p"], generator=gen) * 0.1
     outs = []
-    for dt, odt, layout in ((nv.BF16, g["odt"], g["layout"]), (nv.F32, nv.F32, nv.NHWC)):
-        tdt = torch.bfloat16 if dt == nv.BF16 else torch.float32
+    for dt, odt, layout in ((dt_in, g["odt"], g["layout"]), (nv.F32, nv.F32, nv.NHWC)):
+        tdt = op if dt == dt_in else torch.float32
         xd, wd, bd = x.to(tdt).to(cuda), w.to(tdt).to(cuda), bias.to(cuda)
         if layout == nv.NCHW:
             y = torch.empty(n, g["cv"], ho, wo, dtype=torch.float32, device=cuda)
@@ -115,7 +117,7 @@ def test_every_default_plan_instance_matches_fp32(cuda, default_plan_instances):
         while _plan(g, n) != p and n < g["n"]:
             n += 1
         assert _plan(g, n) == p
-        got, ref = _run_conv(g, n, cuda, nv.BF16)
+        got, ref = _run_conv(g, n, cuda, g["dt"])
         # f32 summation-order noise, plus one rounding of the stored output (bf16: 2^-8, f16: 2^-11 relative)
         rel = {nv.F32: 1e-4, nv.F16: 2 ** -10, nv.BF16: 2 ** -7}[g["odt"]]
         tol = rel * (1 + ref.abs().max().item())
