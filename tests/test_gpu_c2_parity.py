@@ -183,7 +183,10 @@ def test_c2_snr_floor_detects_one_ulp_per_layer(c2, what):
 def test_c2_f16_reconstruction_snr(c2):
     syn = _snr_db(c2["img_syn_f16"], c2["ref"])
     e2e = _snr_db(c2["img_e2e_f16"], c2["ref"])
-    print(f"[c2] f16 synthesis-only SNR {syn:.2f} dB; end-to-end SNR {e2e:.2f} dB")
+    d = (c2["img_syn_f16"] - c2["ref"]).abs()
+    print(f"[c2] f16 synthesis-only SNR {syn:.2f} dB; end-to-end SNR {e2e:.2f} dB; synthesis-only pixel error "
+          f"max {d.max().item():.2e} mean {d.mean().item():.2e} (image range [-1, 1]); fraction of pixels within "
+          f"1e-3: {(d <= 1e-3).float().mean().item():.4f}")
     assert syn > SNR_FLOOR_F16
     assert e2e > SNR_FLOOR_F16 - 6.0  # the split-bf16 encoder's 20 / 262144 boundary flips cost some
 
@@ -201,3 +204,24 @@ def test_c2_f16_psnr_bar(c2, sigma, tol):
           f"end-to-end {d_e2e:+.4f} dB")
     assert abs(d_syn) < tol
     assert abs(d_e2e) < tol
+
+
+def test_c2_f16_floor_detects_one_ulp_per_layer(c2):
+    """The f16 floor is not vacuous: a 2^-11 (one f16 ulp) error in every layer's filtered-lrelu gain pushes the f16
+    synthesis SNR below SNR_FLOOR_F16."""
+    G = c2["G"]
+    layers = [L for L in G.synthesis.layers() if not L.is_torgb]
+    saved = [L.act_gain for L in layers]
+    try:
+        for L in layers:
+            L.act_gain = L.act_gain * (1 + 2 ** -11)
+        G.set_precision("f16")
+        with torch.no_grad():
+            img = G.synthesis(c2["q_or"].to(c2["ref"].device))
+    finally:
+        G.set_precision("fp32")
+        for L, g_ in zip(layers, saved):
+            L.act_gain = g_
+    snr = _snr_db(img, c2["ref"])
+    print(f"[c2] perturbed (gain, 2^-11 per layer): f16 synthesis SNR {snr:.2f} dB")
+    assert snr < SNR_FLOOR_F16

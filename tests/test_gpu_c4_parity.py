@@ -1,7 +1,7 @@
 """Parity of the benched mode on the C4 workload (BASELINE.json configs[3]): HVAE_VGG_Encoder(img_resolution=1024) on
 1024^2 input -> 8-bit uniform quantizer -> SG3-T-1024 synthesis (up-4 layers at 276 / 532 / 1044, the 2098^2
-lrelu grids, the 81 / 51 / 32-channel tail), in bench.py's default precisions (encoder split-bf16 'bf16x3',
-synthesis bf16), at a batch the CPU oracle can afford.
+lrelu grids, the 81 / 51 / 32-channel tail), encoder split-bf16 'bf16x3' with the synthesis in bf16 and in f16 (bench
+--precision bf16 / f16), at a batch the CPU oracle can afford.
 
 Reference path: stylegan3_hvae_full.py:295-329 (compress -> decompress), metric hvae_training.py:368-395.
 The oracle means come from oracle/encoder.py (pinned to the reference's encoder by tests/golden/encoder_full.npz);
@@ -25,9 +25,11 @@ B = 2
 ENC_TOL = 5e-5          # max |means_bench - means_oracle| (8-bit step 2/255 = 0.0078)
 IDX_FRAC = 1e-3         # fraction of the 8-bit indices that may differ (by one) from the oracle's
 HALF_STEP = 1e-4        # a differing index's oracle latent lies within this of a rounding boundary
-SNR_FLOOR_SYN = 36.0    # dB, bf16 SG3-T-1024 synthesis vs the fp32 reference on identical latents
-SNR_FLOOR_E2E = 36.0    # dB, benched encode + quantize + synthesis vs the reference reconstruction
-PSNR_TOL = 0.01         # dB at the 34 dB operating point (north star)
+# per synthesis precision: (synthesis-only SNR floor, end-to-end SNR floor, PSNR tolerances at 34 dB / 46 dB; None =
+# reported only), dB.  bf16 was measured at 43.4 dB SNR, f16 is the CPU-emulated 60 dB class
+FLOORS = {"bf16": (36.0, 36.0, 0.01, None), "f16": (50.0, 48.0, 0.01, 0.01)}
+SNR_FLOOR_SYN = FLOORS["bf16"][0]
+PSNR_TOL = 0.01         # dB (north star)
 
 
 def _snr_db(a, ref):
@@ -54,12 +56,12 @@ def c4(cuda):
         q_or = oe.quantize_uniform(m_or, 8)
         G.set_precision("fp32")
         ref = G.synthesis(q_or.to(cuda))
-        G.set_precision(syn_prec)
-        img_e2e = G.synthesis(q_b)
-        img_syn = G.synthesis(q_or.to(cuda))
+        imgs = {}
+        for prec in FLOORS:
+            G.set_precision(prec)
+            imgs[prec] = (G.synthesis(q_b), G.synthesis(q_or.to(cuda)))
         G.set_precision("fp32")
-    return dict(G=G, m_b=m_b.cpu(), m_or=m_or, q_or=q_or, ref=ref, img_e2e=img_e2e, img_syn=img_syn,
-                syn_prec=syn_prec)
+    return dict(G=G, m_b=m_b.cpu(), m_or=m_or, q_or=q_or, ref=ref, imgs=imgs, syn_prec=syn_prec)
 
 
 def test_c4_bench_indices_vs_oracle(c4):
@@ -77,24 +79,30 @@ def test_c4_bench_indices_vs_oracle(c4):
     assert d.abs().max().item() <= 1 and frac <= IDX_FRAC and (dist <= HALF_STEP).all()
 
 
-def test_c4_reconstruction_snr(c4):
-    syn, e2e = _snr_db(c4["img_syn"], c4["ref"]), _snr_db(c4["img_e2e"], c4["ref"])
-    print(f"[c4] {c4['syn_prec']} SG3-T-1024 synthesis-only SNR {syn:.2f} dB (uint8 PSNR "
-          f"{icm.psnr(c4['img_syn'], c4['ref']):.2f}); end-to-end SNR {e2e:.2f} dB")
-    assert syn > SNR_FLOOR_SYN and e2e > SNR_FLOOR_E2E
+@pytest.mark.parametrize("prec", list(FLOORS))
+def test_c4_reconstruction_snr(c4, prec):
+    e2e_img, syn_img = c4["imgs"][prec]
+    syn, e2e = _snr_db(syn_img, c4["ref"]), _snr_db(e2e_img, c4["ref"])
+    d = (syn_img - c4["ref"]).abs()
+    print(f"[c4] {prec} SG3-T-1024 synthesis-only SNR {syn:.2f} dB (uint8 PSNR {icm.psnr(syn_img, c4['ref']):.2f}); "
+          f"end-to-end SNR {e2e:.2f} dB; synthesis-only pixel error max {d.max().item():.2e} mean {d.mean().item():.2e}")
+    assert syn > FLOORS[prec][0] and e2e > FLOORS[prec][1]
 
 
-@pytest.mark.parametrize("sigma,tol", [(0.039, PSNR_TOL), (0.01, None)])
-def test_c4_psnr_bar(c4, sigma, tol):
+@pytest.mark.parametrize("prec", list(FLOORS))
+@pytest.mark.parametrize("sigma", [0.039, 0.01])
+def test_c4_psnr_bar(c4, sigma, prec):
     g = torch.Generator().manual_seed(78)
     ref = c4["ref"]
     target = ref + (sigma * torch.randn(ref.shape, generator=g)).to(ref.device)
     p_ref = icm.psnr(ref, target)
-    out = {k: icm.psnr(c4[k], target) - p_ref for k in ("img_syn", "img_e2e")}
-    print(f"[c4] sigma={sigma}: PSNR(reference) = {p_ref:.3f} dB; delta synthesis-only {out['img_syn']:+.4f} dB, "
-          f"end-to-end {out['img_e2e']:+.4f} dB")
+    e2e_img, syn_img = c4["imgs"][prec]
+    out = {"syn": icm.psnr(syn_img, target) - p_ref, "e2e": icm.psnr(e2e_img, target) - p_ref}
+    print(f"[c4] {prec} sigma={sigma}: PSNR(reference) = {p_ref:.3f} dB; delta synthesis-only {out['syn']:+.4f} dB, "
+          f"end-to-end {out['e2e']:+.4f} dB")
+    tol = FLOORS[prec][2 if sigma > 0.02 else 3]
     if tol is not None:
-        assert abs(out["img_syn"]) < tol and abs(out["img_e2e"]) < tol
+        assert abs(out["syn"]) < tol and abs(out["e2e"]) < tol
 
 
 def test_c4_snr_floor_detects_one_ulp_per_layer(c4):
@@ -106,7 +114,7 @@ def test_c4_snr_floor_detects_one_ulp_per_layer(c4):
     try:
         for L in layers:
             L.act_gain = L.act_gain * (1 + 2 ** -8)
-        G.set_precision(c4["syn_prec"])
+        G.set_precision("bf16")
         with torch.no_grad():
             img = G.synthesis(c4["q_or"].to(next(G.parameters()).device))
     finally:
