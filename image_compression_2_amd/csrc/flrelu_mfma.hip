@@ -17,7 +17,9 @@
 // workgroups loop over tiles and prefetch the next tile's input (LDS-DMA) while finishing the current one.
 #include "flrelu.h"
 
+#include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace ic2 {
 
@@ -797,6 +799,365 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Strip-streaming variant (round 3).  A work item is a strip: one sample x 32 output columns x 16 channels x a
+// run of consecutive 16-row tiles, walked top to bottom.  Tile t needs lrelu-grid rows 32t .. 32t+41, i.e. grid
+// blocks 2t, 2t+1, 2t+2 of 16 rows, and block 2t+2 is block 0 of tile t+1: the strip computes every grid block
+// once (2 per tile instead of 3) and carries that shared block's vertical-down contribution to the next tile in
+// registers (acc_b).  Its input rows live in an LDS ring of U+1 groups of 16/U rows: block k reads rows
+// 16k/U .. 16k/U+15 (strip-relative; with DELTA = py0 mod U this window covers every tap of the block's rows for
+// every k, so one vertical-up matrix serves all blocks), and after block k's vertical up the group it no longer
+// needs is refilled with the rows block k+2 will need: 16/U new input rows per block (16 / 8 per 16 output rows,
+// up 2 / 4) instead of the tile kernel's 27 / 17.  The horizontal passes are flrelu_mfma2_kernel's.
+template <int U>
+struct FmGeom3 {
+  using G2 = FmGeom2<U, 32>;
+  static constexpr int NINX = G2::NINX;        // 43 (up 2) / 25 (up 4) input columns
+  static constexpr int S = 16 / U;             // input rows per grid block (8 / 4)
+  static constexpr int NG = U + 1;             // ring groups of S rows
+  static constexpr int IN_PITCH = NINX * 8;    // dwords per input row [x][16 ch]; NINX odd
+  static constexpr int GCH = S * NINX * 2;     // 16-B chunks per group
+  static constexpr int NGI = (GCH + 63) / 64;  // 1-KiB DMA instructions per group
+  static constexpr int GRP_DW = NGI * 256;
+  static constexpr int RING_DW = NG * GRP_DW;
+  static constexpr int LDS_DW = RING_DW + G2::V_DW + G2::DT_DW + 16;
+  static_assert(U * S == 16 && NINX % 2 == 1, "geometry");
+  // the surplus columns' reads (x < NW * ceil(NINX / NW)) of the last row of the last group stay in the ring
+  static_assert((NG - 1) * GRP_DW + (S - 1) * IN_PITCH + 8 * 8 * ((NINX + 7) / 8) <= RING_DW, "ring bounds");
+};
+
+template <int U, int DELTA, int NW, bool CL>
+__global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs a, int nitems, int nseg, int seg_len) {
+  constexpr int TOX = 32, NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;
+  using G2 = FmGeom2<U, TOX>;
+  using G = FmGeom3<U>;
+  constexpr int NINX = G::NINX, NBX = G2::NBX, NOB = G2::NOB, S = G::S, NG = G::NG;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW];
+  uint32_t* const ring = lds;
+  uint32_t* const v_img = lds + G::RING_DW;
+  uint32_t* const d_img = v_img + G2::V_DW;
+  float* const taps = reinterpret_cast<float*>(d_img);  // read only before the first strip
+  uint32_t* const ps_lds = d_img + G2::DT_DW;            // the strip's post-scale row (DMA'd with its first rows)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+  // this lane's row in a vertical-up window, as (ring group offset, row in group)
+  const int qoff = (4 * g + tq) / S, roff = (4 * g + tq) % S;
+
+  for (int i = tid; i < FM_TAPS; i += NT) {
+    float v = 0.f;
+    if (i >= 48 && i < 72) v = a.gu[i - 48];
+    else if (i >= 148 && i < 160) v = a.gd[i - 148];
+    else if (i >= 228 && i < 240) v = a.gdg[i - 228];
+    taps[i] = v;
+  }
+
+  // work item w = ((n * tiles_x + tx) * nseg + seg) * cblocks + cb: the channel blocks of one strip run on
+  // consecutive slots of one XCD, so they walk down together and their output stores (32 B of each pixel's
+  // row each) meet in its L2
+  const int slot = fm_xcd_remap(blockIdx.x, gridDim.x);
+  const uint16_t* xin = reinterpret_cast<const uint16_t*>(a.x);
+  auto item_geom = [&](int w, int& n, int& ox0, int& c0, int& t0, int& nt) {
+    const int cb = w % a.cblocks;
+    w /= a.cblocks;
+    const int seg = w % nseg;
+    w /= nseg;
+    const int tx = w % a.tiles_x;
+    n = w / a.tiles_x;
+    ox0 = tx * TOX;
+    c0 = cb * 16;
+    t0 = seg * seg_len;
+    nt = min(seg_len, a.tiles_y - t0);
+  };
+  const int xsy = (int)a.xsy, xsx = (int)a.xsx;  // < 2^31: checked by the launcher (per-sample image < 2 GiB)
+  // group q (strip-relative input rows qS .. qS+S-1 of the item's first tile) -> ring slot q mod NG.  Which
+  // (row, column, half) a lane moves is recomputed per DMA from an opaque copy of the lane id: hoisted out of the
+  // item loop as loop invariants, these per-lane values pushed the kernel past 128 VGPRs into scratch
+  auto load_group = [&](int n, int iy0, int sx0, int c0, int q) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(xin + n * a.xsn + (c0 >> 4) * a.xcb), 0, FM_OOB, 0x00020000);
+    uint32_t* const dst = ring + (q % NG) * G::GRP_DW;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int i = 0; i < (G::NGI + NW - 1) / NW; ++i) {
+      const int k = wave + NW * i;
+      if (k < G::NGI) {
+        const int e = k * 64 + ln;
+        const int pix = e >> 1;
+        const int row = pix / NINX, x = pix - row * NINX;
+        const int iy = iy0 + q * S + row, ix = sx0 + x;
+        const bool ok = e < G::GCH && (unsigned)iy < (unsigned)a.in_h && (unsigned)ix < (unsigned)a.in_w;
+        const uint32_t off = ok ? (uint32_t)((iy * xsy + ix * xsx + (e & 1) * 8) * 2) : FM_OOB;
+        fm_dma16(rs, off, dst + k * 256);
+      }
+    }
+  };
+  // an item's first U+1 groups and its post-scale row (every slot of the ring: issued only once the previous
+  // item's last vertical up is done)
+  auto load_item = [&](int w) __attribute__((always_inline)) {
+    int n, ox0, c0, t0, nt;
+    item_geom(w, n, ox0, c0, t0, nt);
+    const int iy0 = (32 * t0 + DELTA - a.py0) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) load_group(n, iy0, sx0, c0, q);
+    if (a.post_scale != nullptr && wave == NW - 1 && lane < 4) {  // 64 B: post_scale[n][c0 .. c0 + 16)
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.post_scale + (int64_t)n * a.c_p + c0), 0, 64, 0x00020000);
+      fm_dma16(prs, lane * 16, ps_lds);
+    }
+  };
+  if (slot < nitems) load_item(slot);
+  __syncthreads();  // taps
+
+  // filter matrices.  Vertical up: grid row 16k + li of block k from input row kS + 4g + j, tap U(4g + j) +
+  // DELTA - li (the same for every block)
+  fm_h4 gmy, gmx[NBX];
+  {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (4 * g + j) + DELTA - li];
+    gmy = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  const float inv_lim = CL ? 1.f / a.lim : 1.f;
+#pragma unroll
+  for (int t = 0; t < NBX; ++t) {
+    const int w0 = fm_win<U, DELTA, NINX>(16 * t);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)] * inv_lim;
+    gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  fm_h8 gdh01, gdh2, gdq[3];
+  {
+    const float sc = CL ? a.lim : 1.f;
+    auto tap = [&](int blk, int j) { return taps[228 + 16 * blk + 4 * g + j - 2 * li] * sc; };
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = tap(0, j);
+      v[4 + j] = tap(1, j);
+    }
+    gdh01 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = tap(2, j);
+      v[4 + j] = 0.f;
+    }
+    gdh2 = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+    for (int bi = 0; bi < 3; ++bi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = tap(bi, j);
+        v[4 + j] = -tap(bi, j);
+      }
+      gdq[bi] = fm_h8_of(fm_pack4(v[0], v[1], v[2], v[3]), fm_pack4(v[4], v[5], v[6], v[7]));
+    }
+  }
+  fm_h4 gdv[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = taps[148 + 16 * b + 4 * g + j - 2 * li];
+    gdv[b] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
+  }
+  const float slope = a.slope, lim = CL ? 1.f : a.lim;
+  const uint32_t slope2 = fm_h2u(slope, slope), lim2 = fm_h2u(lim, lim), nlim2 = fm_h2u(-lim, -lim);
+  const uint32_t nslope2 = fm_h2u(-slope, -slope);
+  bf16_t* yout = reinterpret_cast<bf16_t*>(a.y);
+  __syncthreads();  // every wave's tap reads are done before the first D store overwrites the table
+
+  bool first = true;
+  for (int w = slot; w < nitems; w += gridDim.x) {
+    int n, ox0, c0, t0, nt;
+    item_geom(w, n, ox0, c0, t0, nt);
+    const int iy0 = (32 * t0 + DELTA - a.py0) / U, sx0 = (ox0 * 2 - a.px0 + DELTA) / U;
+    const bool has_next = w + (int)gridDim.x < nitems;
+    // this wave's DMA of the item's first rows; the previous item's last OCW output stores (issued after that
+    // DMA, always exactly OCW) stay in flight
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
+    first = false;
+    __syncthreads();
+    float4 psv = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (a.post_scale) psv = *reinterpret_cast<const float4*>(ps_lds + 4 * g);
+    const float ps[4] = {psv.x, psv.y, psv.z, psv.w};
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(yout + (int64_t)n * a.out_h * a.out_w * a.c_p + c0), 0, FM_OOB, 0x00020000);
+    const int kend = 2 * nt;  // blocks 0 .. kend
+
+    fm_f4 acc_a[OCW], acc_b[OCW];
+    // grid block k of the item: vertical up (ring -> V), horizontal up / activation / down (V -> D), vertical down
+    // (D -> acc).  MODE 0: block 0, starts acc_b; 1: odd block, acc_a = acc_b + its share; 2: even block >= 2,
+    // finishes acc_a (stored by the caller) and starts acc_b for the next tile.
+    auto block = [&](int k, auto mode_c) __attribute__((always_inline)) {
+      constexpr int MODE = decltype(mode_c)::value;
+      {
+        constexpr int NC = (NINX + NW - 1) / NW;
+        // column x = wave + NW i: one per-lane base per block and immediate offsets.  Columns past NINX - 1 (the
+        // last round's surplus waves) read in-bounds bytes of the ring and are not stored
+        const int q = k + qoff;
+        const uint32_t* rowp = ring + (q % NG) * G::GRP_DW + roff * G::IN_PITCH + 2 * tp + wave * 8;
+        fm_s4 xa[NC];
+        fm_f4 vt[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) xa[i] = fm_tr_read(rowp + i * NW * 8);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          vt[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, xa[i]), gmy,
+                                                        fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t* const vp = v_img + li * G2::V_PITCH + 2 * g + wave * 8;
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          if (i < NC - 1 || wave + NW * i < NINX)
+            *reinterpret_cast<uint2*>(vp + i * NW * 8) = fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
+      }
+      __syncthreads();  // V complete; the ring group k is dead; every wave's vertical down of block k-1 is done
+      // the item's last block: every ring group is dead -> the next item's first rows
+      if (k == kend && has_next) load_item(w + gridDim.x);
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr) {
+        const int row = wave + NW * rr;
+        fm_s4 vb[NBX];
+#pragma unroll
+        for (int tt = 0; tt < NBX; ++tt) {
+          const int w0 = fm_win<U, DELTA, NINX>(16 * tt);
+          vb[tt] = fm_tr_read(v_img + row * G2::V_PITCH + (w0 + 4 * g + tq) * 8 + 2 * tp);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        fm_f4 u[NBX];
+#pragma unroll
+        for (int tt = 0; tt < NBX; ++tt)
+          u[tt] = __builtin_amdgcn_mfma_f32_16x16x16f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[tt]),
+                                                        fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        fm_f4 d[NOB];
+        if constexpr (CL) {
+          fm_h8 qv[NBX];
+#pragma unroll
+          for (int tt = 0; tt < NBX; ++tt) {
+            uint2 p, m;
+            fm_act_split(fm_h2u(u[tt][0], u[tt][1]), fm_h2u(u[tt][2], u[tt][3]), nslope2, p, m);
+            qv[tt] = fm_h8_of(p, m);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int bi = 0; bi < 3; ++bi)
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob)
+              d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qv[2 * ob + bi], gdq[bi],
+                                                             bi == 0 ? fm_f4{0.f, 0.f, 0.f, 0.f} : d[ob], 0, 0, 0);
+        } else {
+          uint2 au[NBX];
+#pragma unroll
+          for (int tt = 0; tt < NBX; ++tt)
+            au[tt] = fm_act_h4(fm_h2u(u[tt][0], u[tt][1]), fm_h2u(u[tt][2], u[tt][3]), slope2, nlim2, lim2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob)
+            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob], au[2 * ob + 1]), gdh01,
+                                                           fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob)
+            d[ob] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fm_h8_of(au[2 * ob + 2], make_uint2(0u, 0u)), gdh2, d[ob],
+                                                           0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          *reinterpret_cast<uint2*>(d_img + row * G2::D_PITCH + (16 * ob + li) * G2::D_XP + 2 * g) =
+              fm_pack4(d[ob][0], d[ob][1], d[ob][2], d[ob][3]);
+      }
+      // the ring group this block's DMA (issued at block k-1's barrier below) filled must have landed before
+      // block k+1's vertical up: wait for it behind the stores of the tile finished at block k-1 (odd k >= 3)
+      if (k >= 1 && k < kend) {
+        if (MODE == 1 && k >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();  // D complete; every wave's horizontal reads of V are done
+      if (k + 2 <= kend) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2 (group k is dead)
+      {
+        fm_s4 da[OCW];
+#pragma unroll
+        for (int i = 0; i < OCW; ++i)
+          da[i] = fm_tr_read(d_img + (4 * g + tq) * G2::D_PITCH + (wave + NW * i) * G2::D_XP + 2 * tp);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < OCW; ++i)
+            acc_b[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[0],
+                                                             fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        } else if constexpr (MODE == 1) {
+#pragma unroll
+          for (int i = 0; i < OCW; ++i)
+            acc_a[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[1], acc_b[i], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < OCW; ++i)
+            acc_a[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[2], acc_a[i], 0, 0, 0);
+          if (k < kend) {
+#pragma unroll
+            for (int i = 0; i < OCW; ++i)
+              acc_b[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, da[i]), gdv[0],
+                                                               fm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+
+    block(0, std::integral_constant<int, 0>{});
+    for (int t = 0; t < nt; ++t) {
+      block(2 * t + 1, std::integral_constant<int, 1>{});
+      block(2 * t + 2, std::integral_constant<int, 2>{});
+      // store tile t0 + t: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox); exactly OCW
+      // buffer stores per wave (out-of-range pixels at the dropped offset FM_OOB)
+      const int gy = 16 * (t0 + t) + li;
+#pragma unroll
+      for (int i = 0; i < OCW; ++i) {
+        const int gx = ox0 + wave + NW * i;
+        const uint32_t off =
+            (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
+        const uint2 v = fm_out4(a.out_f16, acc_a[i][0] * ps[0], acc_a[i][1] * ps[1], acc_a[i][2] * ps[2], acc_a[i][3] * ps[3]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, off, 0, 0);
+      }
+    }
+  }
+}
+
+template <int U, int DELTA, bool CL>
+static void fm3_launch_cl(FlrArgs a, int n, hipStream_t s) {
+  constexpr int TOX = 32, NW = 8;
+  a.tiles_x = (int)ceil_div(a.out_w, TOX);
+  a.tiles_y = (int)ceil_div(a.out_h, 16);
+  a.cblocks = a.c_p / 16;
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma3_kernel<U, DELTA, NW, CL>, 64 * NW, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  // whole-height strips when there are at least two per resident workgroup; otherwise each strip is cut into
+  // segments (one extra grid block each) until there are
+  const int64_t nstrips = (int64_t)n * a.tiles_x * a.cblocks;
+  int nseg = (int)std::min<int64_t>(a.tiles_y, std::max<int64_t>(1, ceil_div(2 * (int64_t)resident, nstrips)));
+  const int seg_len = (int)ceil_div(a.tiles_y, nseg);
+  nseg = (int)ceil_div(a.tiles_y, seg_len);
+  const int nitems = (int)(nstrips * nseg);
+  const int grid = nitems < resident ? nitems : resident;
+  hipLaunchKernelGGL((flrelu_mfma3_kernel<U, DELTA, NW, CL>), dim3((unsigned)grid), dim3(64 * NW), 0, s, a, nitems,
+                     nseg, seg_len);
+}
+
 template <int U, int DELTA, bool CL, int ABL>
 static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
   constexpr int TOX = 32, NW = 8;
@@ -825,7 +1186,13 @@ static void fm2_launch_cl(FlrArgs a, int n, hipStream_t s) {
 template <int U, int DELTA>
 static void fm2_launch(FlrArgs a, int n, hipStream_t s) {
   static const bool split = knob("IC2_FLR_CLSPLIT", 1) != 0;
-  if (split && a.lim >= 0.0625f && a.lim <= 4096.f) {
+  // knob IC2_FLR_STRIP=0: the round-2 tile kernel instead of the strip-streaming one
+  static const bool strip = knob("IC2_FLR_STRIP", 1) != 0;
+  const bool cl = split && a.lim >= 0.0625f && a.lim <= 4096.f;
+  if (strip) {
+    if (cl) fm3_launch_cl<U, DELTA, true>(a, n, s);
+    else fm3_launch_cl<U, DELTA, false>(a, n, s);
+  } else if (cl) {
     fm2_launch_cl<U, DELTA, true, 0>(a, n, s);
   } else {
     fm2_launch_cl<U, DELTA, false, 0>(a, n, s);
@@ -880,8 +1247,10 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
   if ((int64_t)a.out_h * a.out_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // output offsets too
   // the wide (16 x 32) tile for the f16-input synthesis path unless knob IC2_FLR_WIDE=0
   static const bool wide = knob("IC2_FLR_WIDE", 1) != 0;
-  // (only where 32-column tiles pad the output no wider than 16-column ones: not the 36-wide SG3 layers)
-  if (in_f16 && wide && ceil_div(a.out_w, 32) * 32 <= ceil_div(a.out_w, 16) * 16 &&
+  // (only where 32-column tiles pad the output no wider than 16-column ones: not the 36-wide SG3 layers, unless
+  // knob IC2_FLR_WIDE_ALL=1)
+  static const bool wide_all = knob("IC2_FLR_WIDE_ALL", 0) != 0;
+  if (in_f16 && wide && (wide_all || ceil_div(a.out_w, 32) * 32 <= ceil_div(a.out_w, 16) * 16) &&
       (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {
     if (up == 2) {
       if (delta == 0) fm2_launch<2, 0>(a, n, s);

@@ -595,3 +595,34 @@ def test_resize_bilinear(cuda):
     y = ic2.resize_bilinear(x.to(cuda), (16, 16))
     r = F.interpolate(x, size=(16, 16), mode="bilinear", align_corners=False)
     assert _maxdiff(y, r) < 1e-5
+
+
+@pytest.mark.parametrize("layer", [3, 7, 10, 13])
+def test_flrelu_strip_segmentation_invariant(cuda, gen256_bf16_layers, layer):
+    """The strip-streaming filtered lrelu cuts a strip into segments (one extra grid block each) only when a batch
+    has too few strips to fill the chip.  Every grid block is computed from the same input rows with the same taps
+    either way, so a batch of 16 at the layer's real channel count (whole strips) equals the same images run two
+    at a time (segmented strips) bit for bit."""
+    import ctypes
+    L = gen256_bf16_layers[layer]
+    n, c_p = 16, L.cout_p
+    conv = int(L.in_size[0]) + 2
+    s_out = int(L.out_size[0])
+    g = torch.Generator().manual_seed(90 + layer)
+    x = (torch.randn(n, c_p // 16, conv, conv, 16, generator=g) * 2).to(torch.float16).to(cuda)
+    x[:, :, :3, :5] = 300.0
+    ps = (torch.rand(n, c_p, generator=g) + 0.5).to(cuda)
+
+    def run(xs, pss):
+        out = torch.full((xs.shape[0], s_out, s_out, c_p), float("nan"), device=cuda, dtype=torch.bfloat16)
+        nv.call("ic2_flrelu_nhwc16", nv.ptr(xs), nv.ptr(out), nv.F16, nv.BF16, xs.shape[0], c_p, conv, conv, s_out,
+                s_out, L._fu.ctypes.data_as(ctypes.c_void_p), L._fu.shape[0], L._fd.ctypes.data_as(ctypes.c_void_p),
+                L._fd.shape[0], None, L.up_factor, L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0,
+                nv.ptr(pss), nv.stream_of(xs))
+        return out
+
+    full = run(x, ps)
+    parts = torch.cat([run(x[i:i + 2].contiguous(), ps[i:i + 2].contiguous()) for i in range(0, n, 2)])
+    torch.cuda.synchronize()
+    assert torch.isfinite(full.float()).all()
+    assert torch.equal(full, parts)
