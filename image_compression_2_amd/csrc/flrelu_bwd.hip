@@ -25,6 +25,11 @@
 
 namespace ic2 {
 
+int flrelu_bwd_mfma_launch(const void* x, const void* gout, void* gx, const float* oscale, const float* bias,
+                           float* ydot, int64_t ydot_floats, int n, int c_p, int in_h, int in_w, int out_h, int out_w,
+                           const float* gu, const float* gd, int up, int p0, float gain, float slope, float lim,
+                           hipStream_t s);
+
 typedef float bf2v __attribute__((ext_vector_type(2)));
 typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
 
@@ -328,6 +333,20 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
   for (int t = 0; t < 12; ++t) a.gd[t] = 0.f;
   for (int t = 0; t < fu_taps; ++t) a.gu[t] = (flip ? fu[t] : fu[fu_taps - 1 - t]) * (float)up;
   for (int t = 0; t < fd_taps; ++t) a.gd[t] = flip ? fd[t] : fd[fd_taps - 1 - t];
+  // the bf16 training path (f16 x, bf16 gout and gx): the MFMA kernel (flrelu_bwd_mfma.hip) unless knob
+  // IC2_FLRB_MFMA=0; ydot from the stored gx there
+  static const bool mfma = knob("IC2_FLRB_MFMA", 1) != 0;
+  if (mfma && x_dtype == IC2_F16 && g_dtype == IC2_BF16 && gx_dtype == IC2_BF16) {
+    const int64_t need = (int64_t)n * ceil_div(in_h, 16) * ceil_div(in_w, 16) * c_p;
+    IC2_CHECK_ARG(ydot == nullptr || ydot_floats >= need, "flrelu_bwd_nhwc: ydot needs %lld floats", (long long)need);
+    const int rc = flrelu_bwd_mfma_launch(x, gout, gx, oscale, bias, ydot, need, n, c_p, in_h, in_w, out_h, out_w, a.gu,
+                                          a.gd, up, px0, gain, slope, a.lim, as_stream(stream));
+    if (rc == IC2_OK) {
+      IC2_CHECK_LAUNCH("flrelu_bwd_nhwc (mfma)");
+      return IC2_OK;
+    }
+    if (rc != IC2_E_UNSUPPORTED) return rc;
+  }
   // gout phase: R = td - 1 - ph with ph = (-(p0 - tu + 1 - td + 1)) mod down (up % down == 0: same for every tile)
   const int q = px0 - fu_taps + 1 - fd_taps + 1;
   const int ph = ((-q) % down + down) % down;

@@ -412,6 +412,59 @@ def test_flrelu_backward_kernel(cuda, gen256_frozen, li, mode):
     assert e < 1e-3
 
 
+@pytest.mark.parametrize("li", [2, 3, 5, 9, 10, 12])
+@pytest.mark.parametrize("gscale", [1.0, 1e-7])
+def test_flrelu_backward_mfma_kernel(cuda, gen256_frozen, li, gscale):
+    """The bf16 training path's FLR backward on MFMA (flrelu_bwd_mfma.hip: f16 x, bf16 gout, bf16 gx * oscale, the
+    ydot partials of d oscale) on the SG3-T-256 layer geometries (up 2: L2, L9, L12; up 4: L3, L5, L10), against
+    autograd through the oracle's filtered_lrelu in fp64 on the same stored operands.  Bound: the bf16 operands of
+    its four gradient passes (2^-9 each) and the bf16 output; gscale 1e-7 puts dL/dout below the f16 range (the
+    reason the gradient passes are bf16).  Clamp reached on a third of the channels; two samples, so the strip
+    kernel's segments and several channel blocks are covered."""
+    import ctypes
+    L = gen256_frozen.synthesis.layers()[li]
+    c, cp = L.out_channels, L.cout_p
+    n = 2
+    s = int(L.in_size[0]) + L.conv_kernel - 1
+    so = int(L.out_size[0])
+    g = torch.Generator().manual_seed(100 + li)
+    y = torch.randn(n, s, s, c, generator=g) * 3
+    y[..., : c // 3] = y[..., : c // 3] * 60 + 150
+    y = F.pad(y, (0, cp - c)).half()
+    gout = F.pad(torch.randn(n, so, so, c, generator=g) * gscale, (0, cp - c)).bfloat16()
+    os_ = torch.rand(n, cp, generator=g) + 0.5
+    bias = torch.randn(cp, generator=g)
+    yd, gd_, osd, bd = y.to(cuda), gout.to(cuda), os_.to(cuda), bias.to(cuda)
+    dc = torch.empty(n, s, s, cp, device=cuda, dtype=torch.bfloat16)
+    nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, cp, s, s, L.up_factor))
+    ydot = torch.full([nyd], float("nan"), device=cuda)
+    fu, fdn = L._fu, L._fd
+    clamp = float(L.conv_clamp)
+    rc = nv.load().ic2_flrelu_bwd_nhwc_ex(
+        nv.ptr(yd), nv.F16, nv.ptr(gd_), nv.BF16, nv.ptr(dc), nv.BF16, n, cp, s, s, so, so,
+        fu.ctypes.data_as(ctypes.c_void_p), fu.shape[0], fdn.ctypes.data_as(ctypes.c_void_p), fdn.shape[0],
+        L.up_factor, L.down_factor, *L.padding, float(L.act_gain), 0.2, clamp, 0, nv.ptr(osd), nv.ptr(bd),
+        nv.ptr(ydot), nyd, nv.stream_of(yd))
+    assert rc == 0, nv.load().ic2_last_error().decode()
+    torch.cuda.synchronize()
+    yr = y.double()[..., :c].permute(0, 3, 1, 2).requires_grad_(True)
+    _, layers = sg3.layer_table(256)
+    Lr = layers[li]
+    o = sg3.filtered_lrelu(yr, Lr["up_filter"].double(), Lr["down_filter"].double(), up=Lr["up"], down=Lr["down"],
+                           padding=Lr["padding"], clamp=256)
+    o.backward(gout.double()[..., :c].permute(0, 3, 1, 2))
+    ref = yr.grad.permute(0, 2, 3, 1)  # dL/dy, NHWC
+    got = dc.float().cpu()
+    assert torch.isfinite(got).all() and (c == cp or got[..., c:].abs().max().item() == 0.0)
+    e = _rel(got[..., :c], ref * os_.double()[:, None, None, :c])
+    yd_ref = (ref * (y.double()[..., :c] - bias.double()[:c])).sum(dim=(1, 2))
+    yd_got = ydot.view(n, -1, cp).sum(1).cpu()[:, :c]
+    ey = _rel(yd_got, yd_ref)
+    print(f"[flrelu-bwd-mfma L{li} gscale {gscale:g}] rel err gx {e:.2e}, ydot {ey:.2e}")
+    assert e < 1.2e-2
+    assert ey < 2e-2
+
+
 @pytest.mark.parametrize("cp,hw,n", [(512, 38 * 38, 2), (192, 278 * 277, 1), (64, 1000, 3)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_scale_backward_kernel(cuda, cp, hw, n, dtype):
