@@ -13,6 +13,9 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libic2ops.so")
+# diagnostic builds (tools/build_abl.sh) are loaded instead only under IC2_DEV=1 with IC2_DEV_LIB set
+if os.environ.get("IC2_DEV") == "1" and os.environ.get("IC2_DEV_LIB"):
+    LIB_PATH = os.environ["IC2_DEV_LIB"]
 
 F32, BF16, F16, BF16X3 = 0, 1, 2, 3
 ACT_LINEAR, ACT_LRELU = 0, 1

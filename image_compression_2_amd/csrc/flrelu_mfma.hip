@@ -785,6 +785,11 @@ struct FmGeom3 {
   static_assert((NG - 1) * GRP_DW + (S - 1) * IN_PITCH + 8 * 8 * ((NINX + 7) / 8) <= RING_DW, "ring bounds");
 };
 
+// diagnostic builds only (tools/build_abl.sh, wrong results): IC2_FM3_ABL bit 0 skips the ring waits, bit 1 the ring
+// DMAs, bit 2 the horizontal pass
+#ifndef IC2_FM3_ABL
+#define IC2_FM3_ABL 0
+#endif
 template <int U, int DELTA, int NW, bool CL>
 __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs a, int nitems, int nseg, int seg_len) {
   constexpr int TOX = 32, NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;
@@ -982,7 +987,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       // the item's last block: every ring group is dead -> the next item's first rows
       if (k == kend && has_next) load_item(w + gridDim.x);
 #pragma unroll
-      for (int rr = 0; rr < RR; ++rr) {
+      for (int rr = 0; rr < ((IC2_FM3_ABL & 4) ? 0 : RR); ++rr) {
         const int row = wave + NW * rr;
         fm_s4 vb[NBX];
 #pragma unroll
@@ -1036,12 +1041,12 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       }
       // the ring group this block's DMA (issued at block k-1's barrier below) filled must have landed before
       // block k+1's vertical up: wait for it behind the stores of the tile finished at block k-1 (odd k >= 3)
-      if (k >= 1 && k < kend) {
+      if (!(IC2_FM3_ABL & 1) && k >= 1 && k < kend) {
         if (MODE == 1 && k >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();  // D complete; every wave's horizontal reads of V are done
-      if (k + 2 <= kend) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2 (group k is dead)
+      if (!(IC2_FM3_ABL & 2) && k + 2 <= kend) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2
       {
         fm_s4 da[OCW];
 #pragma unroll

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 1120 python -u -m pytest tests -m gpu -x -v -rP --timeout 900 --timeout-method thread \
+timeout -k 10 1120 python -u -m pytest tests -m gpu -v -rP --timeout 900 --timeout-method thread \
   --durations=25 > gpurun_out/r3_suite.log 2>&1
 rc=$?
 grep -E "passed|failed|error" gpurun_out/r3_suite.log | tail -3
