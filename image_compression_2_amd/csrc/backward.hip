@@ -191,14 +191,53 @@ __device__ __forceinline__ float gnb_dz(float yv, float da, float mean, float rs
   return z > 0.f ? da : da * slope;
 }
 
-template <typename TY, typename TD>
-__device__ __forceinline__ float gnb_da(const TD* dout, int nn, int yy, int xx, int h, int w, int c_p, int cc, int pool) {
-  if (!pool) return gld(dout, (((int64_t)nn * h + yy) * w + xx) * c_p + cc);
+
+// 8 consecutive channels per thread (16-B bf16 / 32-B f32 accesses; c_p % 8 == 0: padded to 32 channels)
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+// dL/da of output pixel p (channels cc0 .. cc0 + 7): dout, or a quarter of the pooled gradient (0 on a floor-dropped
+// odd row / column)
+template <typename TD>
+__device__ __forceinline__ void gnb_da8(const TD* dout, int nn, int p, int h, int w, int c_p, int cc0, int pool,
+                                        float (&dv)[8]) {
+  if (!pool) {
+    ld8(dout + ((int64_t)nn * h * w + p) * c_p + cc0, dv);
+    return;
+  }
+  const int yy = p / w, xx = p - (p / w) * w;
   const int oh = h / 2, ow = w / 2;
-  if (yy >= 2 * oh || xx >= 2 * ow) return 0.f;
-  return 0.25f * gld(dout, (((int64_t)nn * oh + yy / 2) * ow + xx / 2) * c_p + cc);
+  if (yy >= 2 * oh || xx >= 2 * ow) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = 0.f;
+    return;
+  }
+  ld8(dout + (((int64_t)nn * oh + yy / 2) * ow + xx / 2) * c_p + cc0, dv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dv[j] *= 0.25f;
 }
 
+// Pass 1: thread = 8 channels (fixed) x pixel lane; per-channel coefficients in registers; two pixels in flight
 template <typename TY, typename TD>
 __global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__ y, const TD* __restrict__ dout, int n,
                                                           int h, int w, int c_p, int c, int groups,
@@ -206,43 +245,65 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float slope, int pool,
                                                           int nchunks, float* __restrict__ part) {
-  // thread -> channel cc = t % CT (+ CT steps), pixel phase t / CT
-  __shared__ float sA[256], sB[256];
+  __shared__ float sAB[256 * 17];  // [thread][8 A, 8 B] (+1: odd row pitch)
   const int hw = h * w;
   const int chunk = blockIdx.x % nchunks, nn = blockIdx.x / nchunks;
   const int p0 = chunk * GNB_CHUNK, p1 = min(hw, p0 + GNB_CHUNK);
-  const int CT = c_p < 256 ? c_p : 256, PS = 256 / CT;
+  const int C8 = c_p >> 3;
+  const int CT = C8 < 256 ? C8 : 256, PS = 256 / CT;
   const int cpg = c / groups;
   const int cl = threadIdx.x % CT, ph = threadIdx.x / CT;
-  for (int cb = 0; cb < c_p; cb += CT) {
-    const int cc = cb + cl;
-    float sa = 0.f, sb = 0.f;
-    if (ph < PS && cc < c) {
-      const int gi = cc / cpg;
-      const float mean = stats[(nn * groups + gi) * 2], rstd = stats[(nn * groups + gi) * 2 + 1];
-      const float gam = gamma[cc], bet = beta[cc];
+  for (int cb = 0; cb < C8; cb += CT) {
+    const int c8 = cb + cl, cc0 = 8 * c8;
+    float sa[8], sb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
+    if (ph < PS && c8 < C8 && cc0 < c) {
+      float mean[8], rstd[8], gam[8], bet[8], valid[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int cc = cc0 + j;
+        const bool ok = cc < c;
+        const int gi = ok ? cc / cpg : 0;
+        mean[j] = stats[(nn * groups + gi) * 2];
+        rstd[j] = stats[(nn * groups + gi) * 2 + 1];
+        gam[j] = ok ? gamma[cc] : 0.f;
+        bet[j] = ok ? beta[cc] : 0.f;
+        valid[j] = ok ? 1.f : 0.f;
+      }
+#pragma unroll 2
       for (int p = p0 + ph; p < p1; p += PS) {
-        const int yy = p / w, xx = p - (p / w) * w;
-        float xhat;
-        const float dz = gnb_dz(gld(y, ((int64_t)nn * hw + p) * c_p + cc),
-                                gnb_da<TY, TD>(dout, nn, yy, xx, h, w, c_p, cc, pool), mean, rstd, gam, bet, slope, xhat);
-        sa += dz;
-        sb += dz * xhat;
+        float yv[8], dv[8];
+        ld8(y + ((int64_t)nn * hw + p) * c_p + cc0, yv);
+        gnb_da8(dout, nn, p, h, w, c_p, cc0, pool, dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float xhat;
+          const float dz = gnb_dz(yv[j], dv[j] * valid[j], mean[j], rstd[j], gam[j], bet[j], slope, xhat);
+          sa[j] += dz;
+          sb[j] += dz * xhat;
+        }
       }
     }
     __syncthreads();
-    sA[threadIdx.x] = sa;
-    sB[threadIdx.x] = sb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sAB[threadIdx.x * 17 + j] = sa[j];
+      sAB[threadIdx.x * 17 + 8 + j] = sb[j];
+    }
     __syncthreads();
-    if (ph == 0 && cc < c_p) {
-      float a = 0.f, b = 0.f;
-      for (int k = 0; k < PS; ++k) {
-        a += sA[k * CT + cl];
-        b += sB[k * CT + cl];
+    if (ph == 0 && c8 < C8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < PS; ++k) {
+          a += sAB[(k * CT + cl) * 17 + j];
+          b += sAB[(k * CT + cl) * 17 + 8 + j];
+        }
+        float* o = part + (((int64_t)nn * c_p + cc0 + j) * nchunks + chunk) * 2;
+        o[0] = a;
+        o[1] = b;
       }
-      float* o = part + (((int64_t)nn * c_p + cc) * nchunks + chunk) * 2;
-      o[0] = a;
-      o[1] = b;
     }
   }
 }
@@ -290,6 +351,7 @@ __global__ void __launch_bounds__(256) gnb_group_kernel(const double* __restrict
   }
 }
 
+// Pass 4: grid (pixel blocks, n); thread = 8 channels (fixed, coefficients in registers) x pixel lane
 template <typename TY, typename TD, typename TO>
 __global__ void __launch_bounds__(256) gnb_apply_kernel(const TY* __restrict__ y, const TD* __restrict__ dout,
                                                         TO* __restrict__ dy, int n, int h, int w, int c_p, int c,
@@ -297,26 +359,43 @@ __global__ void __launch_bounds__(256) gnb_apply_kernel(const TY* __restrict__ y
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float slope, int pool,
                                                         const float* __restrict__ s12) {
-  const int64_t total = (int64_t)n * h * w * c_p;
+  const int hw = h * w, nn = blockIdx.y;
+  const int C8 = c_p >> 3;
+  const int CT = C8 < 256 ? C8 : 256, PS = 256 / CT;
   const int cpg = c / groups;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int cc = (int)(e % c_p);
-    const int64_t pix = e / c_p;
-    const int p = (int)(pix % ((int64_t)h * w));
-    const int nn = (int)(pix / ((int64_t)h * w));
-    float v = 0.f;
-    if (cc < c) {
-      const int gi = cc / cpg;
-      const int sidx = nn * groups + gi;
-      const float mean = stats[2 * sidx], rstd = stats[2 * sidx + 1];
-      const float gam = gamma[cc];
-      const int yy = p / w, xx = p - (p / w) * w;
-      float xhat;
-      const float dz = gnb_dz(gld(y, e), gnb_da<TY, TD>(dout, nn, yy, xx, h, w, c_p, cc, pool), mean, rstd, gam,
-                              beta[cc], slope, xhat);
-      v = rstd * (gam * dz - s12[2 * sidx] - xhat * s12[2 * sidx + 1]);
+  const int cl = threadIdx.x % CT, ph = threadIdx.x / CT;
+  if (ph >= PS) return;
+  for (int cb = 0; cb < C8; cb += CT) {
+    const int c8 = cb + cl, cc0 = 8 * c8;
+    if (c8 >= C8) continue;
+    float mean[8], rstd[8], gam[8], bet[8], s1[8], s2[8], valid[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int cc = cc0 + j;
+      const bool ok = cc < c;
+      const int sidx = nn * groups + (ok ? cc / cpg : 0);
+      mean[j] = stats[2 * sidx];
+      rstd[j] = stats[2 * sidx + 1];
+      gam[j] = ok ? gamma[cc] : 0.f;
+      bet[j] = ok ? beta[cc] : 0.f;
+      s1[j] = s12[2 * sidx];
+      s2[j] = s12[2 * sidx + 1];
+      valid[j] = ok ? 1.f : 0.f;
     }
-    st(dy + e, v);
+#pragma unroll 2
+    for (int p = blockIdx.x * PS + ph; p < hw; p += gridDim.x * PS) {
+      const int64_t e = ((int64_t)nn * hw + p) * c_p + cc0;
+      float yv[8], dv[8], v[8];
+      ld8(y + e, yv);
+      gnb_da8(dout, nn, p, h, w, c_p, cc0, pool, dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float xhat;
+        const float dz = gnb_dz(yv[j], dv[j], mean[j], rstd[j], gam[j], bet[j], slope, xhat);
+        v[j] = valid[j] * rstd[j] * (gam[j] * dz - s1[j] - xhat * s2[j]);
+      }
+      st8(dy + e, v);
+    }
   }
 }
 
@@ -484,6 +563,7 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
                     c <= c_p && groups > 0 && c % groups == 0,
                 "gn_lrelu_pool_bwd: bad arguments");
   IC2_CHECK_ARG(!pool || (h >= 2 && w >= 2), "gn_lrelu_pool_bwd: pooling needs H, W >= 2");
+  IC2_CHECK_ARG(c_p % 8 == 0 && n <= 65535, "gn_lrelu_pool_bwd: c_p must be a multiple of 8 (n <= 65535)");
   IC2_CHECK_ARG(ws_floats >= ic2_gn_lrelu_pool_bwd_floats(n, h, w, c_p, groups), "gn_lrelu_pool_bwd: workspace too small");
   IC2_CHECK_ARG((dtype_y == IC2_F32 || dtype_y == IC2_BF16) && (dtype_dout == IC2_F32 || dtype_dout == IC2_BF16) &&
                     (dtype_dy == IC2_F32 || dtype_dy == IC2_BF16),
@@ -494,7 +574,10 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
   float* s12 = reinterpret_cast<float*>(ab + (int64_t)n * c_p * 2);
   hipStream_t s = as_stream(stream);
   const double ng = (double)h * w * (c / groups);
-  const int64_t total = (int64_t)n * h * w * c_p;
+  // pass 4: (pixel blocks, n); a block covers 256 / min(c_p / 8, 256) pixels per step, ~4 steps per thread
+  const int ps4 = 256 / (c_p / 8 < 256 ? c_p / 8 : 256);
+  const int64_t pblocks = ceil_div(ceil_div((int64_t)h * w, ps4), 4);
+  const dim3 apply_grid((unsigned)(pblocks < 1 ? 1 : (pblocks > 65535 ? 65535 : pblocks)), (unsigned)n);
 #define IC2_GNB(TY, TD)                                                                                          \
   do {                                                                                                           \
     hipLaunchKernelGGL((gnb_partial_kernel<TY, TD>), dim3((unsigned)(n * nchunks)), dim3(256), 0, s, (const TY*)y, \
@@ -505,11 +588,11 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
     hipLaunchKernelGGL(gnb_group_kernel, dim3((unsigned)ceil_div(ng_th, 256)), dim3(256), 0, s, ab, n, c_p, c,     \
                        groups, ng, gamma, s12, dgamma, dbeta);                                                   \
     if (dtype_dy == IC2_F32)                                                                                     \
-      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, float>), dim3(grid_for(total)), dim3(256), 0, s, (const TY*)y,  \
+      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, float>), apply_grid, dim3(256), 0, s, (const TY*)y,             \
                          (const TD*)dout, (float*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,    \
                          s12);                                                                                   \
     else                                                                                                         \
-      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, bf16_t>), dim3(grid_for(total)), dim3(256), 0, s, (const TY*)y, \
+      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, bf16_t>), apply_grid, dim3(256), 0, s, (const TY*)y,            \
                          (const TD*)dout, (bf16_t*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,   \
                          s12);                                                                                   \
   } while (0)
