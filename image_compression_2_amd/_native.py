@@ -82,6 +82,7 @@ _SIGS = {
                                _F, _F, _F, _I, _P, _P, _P, _I64, _P],
     "ic2_scale_bwd_part_floats": [_I, _I, _I],
     "ic2_scale_bwd_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I64, _P],
+    "ic2_scale_nhwc": [_P, _P, _P, _I, _I, _I, _I, _P],
     "ic2_conv3x3_gn_stats_floats": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_conv3x3_gn_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _I64, _P, _I64, _I,
                            _P],

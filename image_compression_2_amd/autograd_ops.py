@@ -280,7 +280,12 @@ class SynthLayerNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, xs, os_, layer, dt):
         n, s_in = x.shape[0], x.shape[1]
-        a = x * xs[:, None, None, :].to(x.dtype)
+        x = x.contiguous()
+        xs32 = xs.detach().float().contiguous()
+        assert xs32.shape == (n, x.shape[3]), (xs32.shape, x.shape)
+        a = torch.empty_like(x)
+        nv.call("ic2_scale_nhwc", nv.ptr(x), nv.ptr(xs32), nv.ptr(a), nv.dtype_code(x.dtype), n, s_in * s_in,
+                x.shape[3], nv.stream_of(x))
         k = layer.conv_kernel
         pad = k - 1
         conv = s_in + 2 * pad - k + 1

@@ -485,6 +485,47 @@ extern "C" int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p) {
   return (int64_t)n * ceil_div(hw, sb_chunk_pix(n, hw)) * c_p;
 }
 
+// a = x * xscale[n][c]: grid (pixel blocks, n), thread = 8 channels (scale in registers) x pixel lane
+template <typename T>
+__global__ void __launch_bounds__(256) scale_fwd_kernel(const T* __restrict__ x, const float* __restrict__ xs,
+                                                        T* __restrict__ a, int hw, int c_p) {
+  const int nn = blockIdx.y, C8 = c_p >> 3;
+  const int CT = C8 < 256 ? C8 : 256, PS = 256 / CT;
+  const int cl = threadIdx.x % CT, ph = threadIdx.x / CT;
+  if (ph >= PS) return;
+  for (int c8 = cl; c8 < C8; c8 += CT) {
+    float sc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sc[j] = xs[(int64_t)nn * c_p + 8 * c8 + j];
+#pragma unroll 2
+    for (int p = blockIdx.x * PS + ph; p < hw; p += gridDim.x * PS) {
+      const int64_t e = ((int64_t)nn * hw + p) * c_p + 8 * c8;
+      float v[8];
+      ld8(x + e, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= sc[j];
+      st8(a + e, v);
+    }
+  }
+}
+
+extern "C" int ic2_scale_nhwc(const void* x, const float* xscale, void* a, int dtype, int n, int hw, int c_p,
+                              void* stream) {
+  IC2_CHECK_ARG(x && xscale && a && n > 0 && n <= 65535 && hw > 0 && c_p > 0 && c_p % 8 == 0, "scale_nhwc: bad arguments");
+  const int ps = 256 / (c_p / 8 < 256 ? c_p / 8 : 256);
+  const int64_t pb = ceil_div(ceil_div((int64_t)hw, ps), 4);
+  const dim3 grid((unsigned)(pb < 1 ? 1 : (pb > 65535 ? 65535 : pb)), (unsigned)n);
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(scale_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, xscale, (float*)a, hw, c_p);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(scale_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, xscale, (bf16_t*)a, hw, c_p);
+  else
+    IC2_CHECK_ARG(false, "scale_nhwc: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("scale_nhwc");
+  return IC2_OK;
+}
+
 extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw,
                                   int c_p, float* part, int64_t part_floats, void* stream) {
   IC2_CHECK_ARG(da && x && xscale && dx && part && n > 0 && hw > 0 && c_p > 0 && c_p % 2 == 0 && c_p <= 512,

@@ -430,59 +430,55 @@ static void fbm_launch(FlrBwdMArgs a, int n, hipStream_t s) {
 __global__ void __launch_bounds__(256) fb_ydot_kernel(const uint16_t* __restrict__ dc, const uint16_t* __restrict__ x,
                                                       const float* __restrict__ oscale, const float* __restrict__ bias,
                                                       float* __restrict__ part, int hw, int c_p, int nchunks, int per) {
-  // thread t: channel pair (t mod pairs) of pixels p0 + t / pairs, stepping by 256 / pairs; four pixels in flight per
-  // thread (independent accumulators); fixed-order reduction over the pixel lanes in LDS
-  __shared__ fm_f2 red[256];
+  // thread t: channel octet (t mod octs) of pixels p0 + t / octs, stepping by 256 / octs (16-B loads); two pixels in
+  // flight per thread; fixed-order reduction over the pixel lanes in LDS
+  __shared__ float red[256 * 9];
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int p0 = chunk * per, p1 = min(hw, p0 + per);
-  for (int cbase = 0; cbase < c_p; cbase += 512) {
-    const int pairs = min(256, (c_p - cbase) >> 1);
-    const int lanes = 256 / pairs;  // pixel lanes (pairs is a power of two times 16: c_p % 32 == 0)
+  const int C8 = c_p >> 3;
+  for (int cbase = 0; cbase < C8; cbase += 256) {
+    const int octs = min(256, C8 - cbase);
+    const int lanes = 256 / octs;
     const int t = threadIdx.x;
-    const int cp2 = t % pairs, pl = t / pairs;
-    const int c = cbase + 2 * cp2;
-    fm_f2 acc = fm_f2{0.f, 0.f};
+    const int o8 = t % octs, pl = t / octs;
+    const int c = 8 * (cbase + o8);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
     if (pl < lanes) {
-      const float b0 = bias ? bias[c] : 0.f, b1 = bias ? bias[c + 1] : 0.f;
+      float b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = bias ? bias[c + j] : 0.f;
       const int64_t base = (int64_t)n * hw * c_p + c;
-      fm_f2 a4[4] = {fm_f2{0.f, 0.f}, fm_f2{0.f, 0.f}, fm_f2{0.f, 0.f}, fm_f2{0.f, 0.f}};
-      int p = p0 + pl;
-      for (; p + 3 * lanes < p1; p += 4 * lanes) {
-        uint32_t dv[4], xv[4];
+#pragma unroll 2
+      for (int p = p0 + pl; p < p1; p += lanes) {
+        const uint4 dv = *reinterpret_cast<const uint4*>(dc + base + (int64_t)p * c_p);
+        const uint4 xv = *reinterpret_cast<const uint4*>(x + base + (int64_t)p * c_p);
+        const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          dv[u] = *reinterpret_cast<const uint32_t*>(dc + base + (int64_t)(p + u * lanes) * c_p);
-          xv[u] = *reinterpret_cast<const uint32_t*>(x + base + (int64_t)(p + u * lanes) * c_p);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const fm_h2 xh = __builtin_bit_cast(fm_h2, xv[u]);
-          a4[u].x += __uint_as_float(dv[u] << 16) * ((float)xh.x - b0);
-          a4[u].y += __uint_as_float(dv[u] & 0xffff0000u) * ((float)xh.y - b1);
+        for (int k = 0; k < 4; ++k) {
+          const fm_h2 xh = __builtin_bit_cast(fm_h2, xw[k]);
+          acc[2 * k] += __uint_as_float(dw[k] << 16) * ((float)xh.x - b[2 * k]);
+          acc[2 * k + 1] += __uint_as_float(dw[k] & 0xffff0000u) * ((float)xh.y - b[2 * k + 1]);
         }
       }
-      for (; p < p1; p += lanes) {
-        const uint32_t dv = *reinterpret_cast<const uint32_t*>(dc + base + (int64_t)p * c_p);
-        const fm_h2 xh = __builtin_bit_cast(fm_h2, *reinterpret_cast<const uint32_t*>(x + base + (int64_t)p * c_p));
-        a4[0].x += __uint_as_float(dv << 16) * ((float)xh.x - b0);
-        a4[0].y += __uint_as_float(dv & 0xffff0000u) * ((float)xh.y - b1);
-      }
-      acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     }
     __syncthreads();
-    red[t] = acc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t * 9 + j] = acc[j];
     __syncthreads();
-    if (t < pairs) {
-      fm_f2 sum = fm_f2{0.f, 0.f};
-      for (int l = 0; l < lanes; ++l) sum += red[l * pairs + t];
-      if (oscale) {
-        const float o0 = oscale[(int64_t)n * c_p + c], o1 = oscale[(int64_t)n * c_p + c + 1];
-        sum.x = o0 != 0.f ? sum.x / o0 : 0.f;
-        sum.y = o1 != 0.f ? sum.y / o1 : 0.f;
-      }
+    if (t < octs) {
       float* pp = part + ((int64_t)n * nchunks + chunk) * c_p + c;
-      pp[0] = sum.x;
-      pp[1] = sum.y;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float sum = 0.f;
+        for (int l = 0; l < lanes; ++l) sum += red[(l * octs + t) * 9 + j];
+        if (oscale) {
+          const float o = oscale[(int64_t)n * c_p + c + j];
+          sum = o != 0.f ? sum / o : 0.f;
+        }
+        pp[j] = sum;
+      }
     }
   }
 }

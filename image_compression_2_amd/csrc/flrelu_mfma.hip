@@ -786,7 +786,7 @@ struct FmGeom3 {
 };
 
 // diagnostic builds only (tools/build_abl.sh, wrong results): IC2_FM3_ABL bit 0 skips the ring waits, bit 1 the ring
-// DMAs, bit 2 the horizontal pass
+// DMAs, bit 2 the horizontal pass, bit 3 the vertical up, bit 4 the vertical down, bit 5 the two in-block barriers
 #ifndef IC2_FM3_ABL
 #define IC2_FM3_ABL 0
 #endif
@@ -961,7 +961,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
     // finishes acc_a (stored by the caller) and starts acc_b for the next tile.
     auto block = [&](int k, auto mode_c) __attribute__((always_inline)) {
       constexpr int MODE = decltype(mode_c)::value;
-      {
+      if constexpr (!(IC2_FM3_ABL & 8)) {
         constexpr int NC = (NINX + NW - 1) / NW;
         // column x = wave + NW i: one per-lane base per block and immediate offsets.  Columns past NINX - 1 (the
         // last round's surplus waves) read in-bounds bytes of the ring and are not stored
@@ -983,7 +983,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
           if (i < NC - 1 || wave + NW * i < NINX)
             *reinterpret_cast<uint2*>(vp + i * NW * 8) = fm_pack4(vt[i][0], vt[i][1], vt[i][2], vt[i][3]);
       }
-      __syncthreads();  // V complete; the ring group k is dead; every wave's vertical down of block k-1 is done
+      if constexpr (!(IC2_FM3_ABL & 32)) __syncthreads();  // V complete; the ring group k is dead; v-down k-1 done
       // the item's last block: every ring group is dead -> the next item's first rows
       if (k == kend && has_next) load_item(w + gridDim.x);
 #pragma unroll
@@ -1045,9 +1045,9 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
         if (MODE == 1 && k >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      __syncthreads();  // D complete; every wave's horizontal reads of V are done
+      if constexpr (!(IC2_FM3_ABL & 32)) __syncthreads();  // D complete; every wave's horizontal reads of V are done
       if (!(IC2_FM3_ABL & 2) && k + 2 <= kend) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2
-      {
+      if constexpr (!(IC2_FM3_ABL & 16)) {
         fm_s4 da[OCW];
 #pragma unroll
         for (int i = 0; i < OCW; ++i)

@@ -36,8 +36,11 @@ def kl_divergence(means, logvars, w_avg):
 
 
 def make_optimizer(encoder, lr=1e-4):
-    """The reference's optimizer (:484)."""
-    return torch.optim.Adam(encoder.parameters(), lr=lr, betas=(0.9, 0.999))
+    """The reference's optimizer (:484), as one fused multi-tensor kernel per step on the device (the same update
+    rule; torch's per-parameter path launched ~8 elementwise kernels per encoder tensor)."""
+    params = list(encoder.parameters())
+    fused = all(p.is_cuda for p in params)
+    return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), fused=fused or None)
 
 
 def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_weight=0.8, kl_weight=0.01,

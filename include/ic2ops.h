@@ -353,6 +353,11 @@ int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p);
 int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw, int c_p,
                        float* part, int64_t part_floats, void* stream);
 
+/* Its forward on the training path (SynthLayerNHWC; inference folds xscale into the producer's epilogue):
+ * a[n][p][c] = x[n][p][c] * xscale[n][c], NHWC f32 / bf16, c_p % 8 == 0.  Replaces the reference's
+ * `x * styles` broadcast inside modulated_conv2d (SG3-public, called at stylegan3_hvae_full.py:274). */
+int ic2_scale_nhwc(const void* x, const float* xscale, void* a, int dtype, int n, int hw, int c_p, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

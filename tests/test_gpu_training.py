@@ -485,3 +485,19 @@ def test_scale_backward_kernel(cuda, cp, hw, n, dtype):
     dxs = part.view(n, -1, cp).sum(1).cpu().double()
     ref = (da.double() * x.double()).sum(1)
     assert _rel(dxs, ref) < 1e-5
+
+
+@pytest.mark.parametrize("cp,hw,n", [(512, 38 * 38, 2), (192, 278 * 277, 1), (96, 1000, 3)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_scale_forward_kernel(cuda, cp, hw, n, dtype):
+    """ic2_scale_nhwc (the training path's a = x * xscale[n][c]): f32 exact, bf16 the product of the f32 scale and the
+    bf16 input rounded once."""
+    g = torch.Generator().manual_seed(cp + 1)
+    x = torch.randn(n, hw, cp, generator=g).to(dtype)
+    xs = torch.randn(n, cp, generator=g)
+    xd, xsd = x.to(cuda), xs.to(cuda)
+    a = torch.empty_like(xd)
+    nv.call("ic2_scale_nhwc", nv.ptr(xd), nv.ptr(xsd), nv.ptr(a), nv.dtype_code(dtype), n, hw, cp, nv.stream_of())
+    ref = (x.float() * xs[:, None, :]).to(dtype)  # one f32 product, rounded once (exact for f32)
+    assert torch.equal(a.cpu(), ref)
+
