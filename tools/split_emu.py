@@ -20,8 +20,18 @@ def rnd(t, dt): return t.to(dt).to(torch.float64)
 def split(t, dt):
     hi = t.to(dt).to(torch.float64); lo = (t.double() - hi).to(dt).to(torch.float64); return hi, lo
 
+CONV_IDX = [0]
+
+
 def make_conv(mode):
+    base = mode
+    if mode.startswith('mix'):   # mixK: the first K convs (from_rgb = 0, block0 conv1 = 1, ...) in bf16, the rest split
+        k = int(mode[3:])
     def conv(x, w, b):
+        mode = base
+        if base.startswith('mix'):
+            mode = 'bf16' if CONV_IDX[0] < k else 'split_bf16'
+            CONV_IDX[0] += 1
         if mode == 'fp64':
             y = F.conv2d(x.double(), w.double(), b.double(), padding=1)
         elif mode in ('bf16', 'f16'):
@@ -44,8 +54,12 @@ def make_conv(mode):
     return conv
 
 def enc_forward(mode):
+    CONV_IDX[0] = 0
     conv = make_conv(mode)
     store = (lambda t: t.to(torch.bfloat16).float()) if mode == 'bf16' else (lambda t: t)
+    if mode.startswith('mix'):  # activations stored bf16 while the convs consuming them are bf16
+        k = int(mode[3:])
+        store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] < k else t
     h = store(conv(x, sd['from_rgb.weight'], sd['from_rgb.bias']))
     feats = {}
     for i in range(10):
