@@ -790,6 +790,10 @@ struct FmGeom3 {
 #ifndef IC2_FM3_ABL
 #define IC2_FM3_ABL 0
 #endif
+// ring DMA of block k+2 issued right after block k's vertical-up barrier (1) or after its horizontal pass (0)
+#ifndef FM3_EARLY
+#define FM3_EARLY 1
+#endif
 template <int U, int DELTA, int NW, bool CL>
 __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs a, int nitems, int nseg, int seg_len) {
   constexpr int TOX = 32, NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;
@@ -840,6 +844,9 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
   // group q (strip-relative input rows qS .. qS+S-1 of the item's first tile) -> ring slot q mod NG.  Which
   // (row, column, half) a lane moves is recomputed per DMA from an opaque copy of the lane id: hoisted out of the
   // item loop as loop invariants, these per-lane values pushed the kernel past 128 VGPRs into scratch
+  // this wave's DMA instructions per ring group (wave-uniform; at most 2: the wait counts above)
+  const int my_dma = wave < G::NGI ? (G::NGI - 1 - wave) / NW + 1 : 0;
+  static_assert((G::NGI + NW - 1) / NW <= 2, "ring group DMA per wave");
   auto load_group = [&](int n, int iy0, int sx0, int c0, int q) __attribute__((always_inline)) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(xin + n * a.xsn + (c0 >> 4) * a.xcb), 0, FM_OOB, 0x00020000);
@@ -986,6 +993,10 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       if constexpr (!(IC2_FM3_ABL & 32)) __syncthreads();  // V complete; the ring group k is dead; v-down k-1 done
       // the item's last block: every ring group is dead -> the next item's first rows
       if (k == kend && has_next) load_item(w + gridDim.x);
+      // the rows block k+2 needs go out now, into the slot of group k (every wave's vertical up of block k is done):
+      // they land behind this block's horizontal pass and vertical down and the next block's vertical up
+      const bool dma = !(IC2_FM3_ABL & 2) && k + 2 <= kend;
+      if (FM3_EARLY && dma) load_group(n, iy0, sx0, c0, k + U + 1);
 #pragma unroll
       for (int rr = 0; rr < ((IC2_FM3_ABL & 4) ? 0 : RR); ++rr) {
         const int row = wave + NW * rr;
@@ -1042,11 +1053,23 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       // the ring group this block's DMA (issued at block k-1's barrier below) filled must have landed before
       // block k+1's vertical up: wait for it behind the stores of the tile finished at block k-1 (odd k >= 3)
       if (!(IC2_FM3_ABL & 1) && k >= 1 && k < kend) {
-        if (MODE == 1 && k >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // block k-1's ring DMA must have landed (block k+1 reads it); younger: the stores of a tile finished at block
+        // k-1 (odd k >= 3: exactly OCW) and, issued early, this block's own DMA (this wave's share, uniform)
+        const bool st = MODE == 1 && k >= 3;
+        const int nd = FM3_EARLY && dma ? my_dma : 0;
+        if (nd == 0) {
+          if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (nd == 1) {
+          if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW + 1) : "memory");
+          else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        } else {
+          if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW + 2) : "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
       }
       if constexpr (!(IC2_FM3_ABL & 32)) __syncthreads();  // D complete; every wave's horizontal reads of V are done
-      if (!(IC2_FM3_ABL & 2) && k + 2 <= kend) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2
+      if (!FM3_EARLY && dma) load_group(n, iy0, sx0, c0, k + U + 1);  // rows of block k+2
       if constexpr (!(IC2_FM3_ABL & 16)) {
         fm_s4 da[OCW];
 #pragma unroll

@@ -8,8 +8,11 @@ for abl in "$@"; do
   objs=""
   for f in image_compression_2_amd/csrc/*.hip; do
     o=$d/$(basename $f .hip).o
+    if [ "$(basename $f)" != flrelu_mfma.hip ] && [ ! -f $o ] && [ -f image_compression_2_amd/_build/$(basename $f .hip).o ]; then
+      cp image_compression_2_amd/_build/$(basename $f .hip).o $o   # only flrelu_mfma.hip differs
+    fi
     if [ "$(basename $f)" = flrelu_mfma.hip ] || [ ! -f $o ]; then
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Wno-unused-result -DIC2_FM3_ABL=$abl \
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Wno-unused-result -DIC2_FM3_ABL=$abl $EXTRA \
         $( [ "$(basename $f)" = flrelu_mfma.hip ] && echo "-mllvm -amdgpu-mfma-vgpr-form" ) \
         $( [ "$(basename $f)" = flrelu_bwd.hip ] && echo "-mllvm -pragma-unroll-threshold=200000" ) -c $f -o $o &
     fi
