@@ -35,22 +35,6 @@ struct WgradArgs {
   int j_tiles;  // kh * kw * cin_p / 64
 };
 
-template <typename T>
-__device__ __forceinline__ void wg_load_row(const T* src, bool ok, T* dst);
-
-template <>
-__device__ __forceinline__ void wg_load_row<bf16_t>(const bf16_t* src, bool ok, bf16_t* dst) {
-  const uint4 v = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0u, 0u, 0u, 0u);
-  *reinterpret_cast<uint4*>(dst) = v;  // 8 elements
-}
-template <>
-__device__ __forceinline__ void wg_load_row<float>(const float* src, bool ok, float* dst) {
-  const float4 a = ok ? reinterpret_cast<const float4*>(src)[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 b = ok ? reinterpret_cast<const float4*>(src)[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-  reinterpret_cast<float4*>(dst)[0] = a;
-  reinterpret_cast<float4*>(dst)[1] = b;
-}
-
 __device__ __forceinline__ wg_s4 wg_tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) wg_s4*)p);
 }
@@ -83,7 +67,11 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int ch = c0; ch < c1; ++ch) {
+  // the next chunk's rows are loaded into registers while this chunk's MFMAs run (the loop was one exposed global
+  // load round trip per 32 pixels)
+  constexpr int NV = sizeof(T) / 2;  // 16-B registers per 8-element row segment
+  uint4 vd[NV], vx[NV];
+  auto load_chunk = [&](int ch) {
     const int p = ch * WG_KP + r;
     const bool okp = p < a.P;
     const int pp = okp ? p : 0;
@@ -92,12 +80,26 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
     const int oy = rem / a.wo, ox = rem - (rem / a.wo) * a.wo;
     const int iy = oy - a.pad + ky, ix = ox - a.pad + kx;
     const bool okx = okp && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    __syncthreads();  // previous chunk's fragment reads done
     const bool oko = okp && o0 + seg * 8 < a.cout_p, oki = okx && ci0 + seg * 8 < a.cin_p;
-    wg_load_row<T>(dyg + (int64_t)pp * a.cout_p + (oko ? o0 + seg * 8 : 0), oko, sdy + r * WG_PITCH + seg * 8);
-    wg_load_row<T>(xg + (((int64_t)nn * a.h + (okx ? iy : 0)) * a.w + (okx ? ix : 0)) * a.cin_p + (oki ? ci0 + seg * 8 : 0),
-                   oki, sx + r * WG_PITCH + seg * 8);
+    const uint4* sd = reinterpret_cast<const uint4*>(dyg + (int64_t)pp * a.cout_p + (oko ? o0 + seg * 8 : 0));
+    const uint4* sxp = reinterpret_cast<const uint4*>(
+        xg + (((int64_t)nn * a.h + (okx ? iy : 0)) * a.w + (okx ? ix : 0)) * a.cin_p + (oki ? ci0 + seg * 8 : 0));
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      vd[v] = oko ? sd[v] : make_uint4(0u, 0u, 0u, 0u);
+      vx[v] = oki ? sxp[v] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  if (c0 < c1) load_chunk(c0);
+  for (int ch = c0; ch < c1; ++ch) {
+    __syncthreads();  // previous chunk's fragment reads done
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      reinterpret_cast<uint4*>(sdy + r * WG_PITCH + seg * 8)[v] = vd[v];
+      reinterpret_cast<uint4*>(sx + r * WG_PITCH + seg * 8)[v] = vx[v];
+    }
     __syncthreads();
+    if (ch + 1 < c1) load_chunk(ch + 1);
     if constexpr (sizeof(T) == 2) {
       // A[m = o][k = p]: lane (g, li) = pixels 8g .. 8g+7 of column o; two transposed reads of 4 rows each.
       // Within a 16-lane group, lane (tq = li / 4, tp = li % 4) reads row base + tq, elements 4 tp .. 4 tp + 3.
@@ -165,9 +167,9 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 
 static int wgrad_splits(const WgradArgs& a) {
   const int64_t tiles = ceil_div(a.cout_p, WG_BO) * a.j_tiles;
-  int64_t sp = ceil_div(2048, tiles);
+  int64_t sp = ceil_div(4096, tiles);  // ~16 workgroups per CU: the shallow layers have only 9-18 tiles
   if (sp > a.chunks) sp = a.chunks;
-  if (sp > 64) sp = 64;
+  if (sp > 256) sp = 256;
   return (int)(sp < 1 ? 1 : sp);
 }
 
