@@ -376,15 +376,25 @@ __global__ void __launch_bounds__(256) gap_partial_kernel(const T* __restrict__ 
   part[((int64_t)nn * nchunks + chunk) * c_p + ch] = s;
 }
 
+// grid (ceil(c / 16), n): 16 channels x 16 chunk lanes per block (the 1024^2 encoder's fine projector has 256+
+// chunks per image: one thread per (n, c) summing them in sequence was a serial chain of loads); each lane sums
+// chunks lane, lane + 16, ... and the lanes combine in a fixed order (deterministic)
 __global__ void __launch_bounds__(256) gap_finalize_kernel(const float* __restrict__ part, int n, int c_p, int c,
                                                            int nchunks, int hw, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)n * c) return;
-  const int ch = (int)(i % c);
-  const int64_t nn = i / c;
+  __shared__ float red[16][17];
+  const int nn = blockIdx.y, cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + cl;
   float s = 0.f;
-  for (int k = 0; k < nchunks; ++k) s += part[(nn * nchunks + k) * c_p + ch];
-  out[i] = s / (float)hw;
+  if (ch < c)
+    for (int k = lane; k < nchunks; k += 16) s += part[((int64_t)nn * nchunks + k) * c_p + ch];
+  red[lane][cl] = s;
+  __syncthreads();
+  if (lane == 0 && ch < c) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) t += red[l][cl];
+    out[(int64_t)nn * c + ch] = t / (float)hw;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -861,7 +871,7 @@ extern "C" int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int 
     hipLaunchKernelGGL(gap_partial_kernel<bf16x3_t>, grid, dim3(256), 0, s, (const bf16x3_t*)x, hw, c_p, nchunks, part);
   else
     IC2_CHECK_ARG(false, "global_avg_pool: bad dtype");
-  hipLaunchKernelGGL(gap_finalize_kernel, dim3((unsigned)ceil_div((int64_t)n * c, 256)), dim3(256), 0, s, part, n, c_p,
+  hipLaunchKernelGGL(gap_finalize_kernel, dim3((unsigned)ceil_div(c, 16), (unsigned)n), dim3(256), 0, s, part, n, c_p,
                      c, nchunks, hw, out);
   IC2_CHECK_LAUNCH("global_avg_pool");
   return IC2_OK;

@@ -1,10 +1,10 @@
 #!/bin/bash
 # round-3 bench evidence: C2 in every precision, C4, C2g, C5, and rocprofv3 kernel traces of C2 and C4
 set -o pipefail
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r3e
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/$1
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 tag=${1:-r3e}
-o=gpurun_out/r3e
+o=gpurun_out/$1
 run() {  # name, args...
   local n=$1; shift
   timeout -k 10 300 python bench.py "$@" --out $o/${tag}_$n.json > $o/${tag}_$n.log 2>&1 || { tail -20 $o/${tag}_$n.log; exit 1; }
