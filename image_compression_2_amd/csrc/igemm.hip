@@ -729,7 +729,7 @@ __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((
 // HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
 // past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
 // chain, ~60 SALU per step) and a wait count that depends only on the tap
-template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false>
+template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false, int TPB = 1>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = H4<I, J, WGO, WGP, TW, NS, HB>;
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
@@ -822,6 +822,64 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
 #pragma unroll
   for (int k = 0; k < HPW; ++k)
     if (wid + 4 * k < G::NHI) issue_h1(0, k);
+  if constexpr (TPB > 1) {
+    // TPB taps per barrier: step s computes taps TPB*s .. TPB*s+TPB-1 (with TPB = 2 a pair may straddle two channel
+    // blocks; both halos are resident).  Slabs of step s+L are issued at step s into the ring positions step s-1
+    // read, so the ring holds L+1 steps; the DMA lookahead in MFMA cycles is TPB*L taps (the one-tap ring: LA-1).
+    static_assert(HB && NS % TPB == 0 && NS >= 2 * TPB && (TPB == 2 || TPB == 3), "TPB: halo burst, ring of steps");
+    constexpr int L = NS / TPB - 1;
+    const int nst = (nq + TPB - 1) / TPB;
+    auto burst_at = [&](int st) {  // block cb0+1's halo: first step with no tap of block cb0-1
+      const int t0 = TPB * st, cb0 = t0 / 9;
+      return t0 - cb0 * 9 < TPB && cb0 + 1 < CB;
+    };
+#pragma unroll
+    for (int t = 0; t < TPB * L; ++t) issue_w(t);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI) : "memory");  // halo 0 and step 0's slabs landed
+    for (int s = 0; s < nst; ++s) {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const int t0 = TPB * s;
+#pragma unroll
+      for (int u = 0; u < TPB; ++u) issue_w(t0 + u + TPB * L);
+      const bool burst = burst_at(s);  // first read >= 3 steps later
+      if (burst) issue_hb(t0 / 9 + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 af[TPB][I], bfr[TPB][J];
+#pragma unroll
+      for (int u = 0; u < TPB; ++u) {
+        const int t = t0 + u, cb = t / 9, tap = t - cb * 9;
+        // the swizzle depends on the absolute halo row: the tap shift goes into the row, not the base pointer
+        const int sh = (tap / 3) * G::HW + tap % 3;
+        const char* hb = hal + (cb & 1) * G::HALO_B;
+        const char* wl = wsl + (t % NS) * G::WS_B;
+#pragma unroll
+        for (int j = 0; j < J; ++j) bfr[u][j] = *reinterpret_cast<const bf16x8*>(hb + h4_off(brow[j] + sh, fh));
+#pragma unroll
+        for (int i = 0; i < I; ++i) af[u][i] = *reinterpret_cast<const bf16x8*>(wl + h4_off(obase + i * 16 + fr, fh));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      if (live) {
+#pragma unroll
+        for (int u = 0; u < TPB; ++u) {
+          if (u == 0 || t0 + u < nq) {  // the tail step of an odd tap count has one tap
+#pragma unroll
+            for (int i = 0; i < I; ++i)
+#pragma unroll
+              for (int j = 0; j < J; ++j) acc[i][j] = mfma32<F16>(af[u][i], bfr[u][j], acc[i][j]);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // step s+1's slabs landed (issued at step s+1-L); a burst of the last L steps may stay in flight (issued after
+      // its step's slabs; bursts are >= 3 steps apart)
+      const bool recent = burst || (L > 1 && s > 0 && burst_at(s - 1));
+      if (recent) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI + HPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI) : "memory");
+    }
+  } else {
 #pragma unroll
   for (int t = 0; t < LA; ++t) issue_w(t);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");  // halo 0 and slab 0 landed
@@ -870,6 +928,7 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * NWI) : "memory");
     }
   }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail (zero-size) DMAs before the epilogue
 
   const int hw = a.ho * a.wo;
@@ -906,24 +965,27 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
                                                                                                 int tx, int ty) { \
     hg4_body<I, J, WGO, WGP, TW, NS, false, true>(a, tx, ty);                                                    \
   }
-#define IC2_HG4_KERNEL_HB(name, I, J, WGO, WGP, TW, NS)                                                          \
-  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
-                                                                                          int ty) {            \
-    hg4_body<I, J, WGO, WGP, TW, NS, true>(a, tx, ty);                                                           \
-  }                                                                                                              \
-  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name##_f16(IgemmArgs a,     \
-                                                                                                int tx, int ty) { \
-    hg4_body<I, J, WGO, WGP, TW, NS, true, true>(a, tx, ty);                                                     \
-  }
-// the launch plan's instances: halo-burst (HB) kernels for 32-wide pixel tiles, 4-slab rings for 16-wide ones
+// the launch plan's instances: 4-slab one-tap rings for 16-wide pixel tiles, multi-tap halo-burst kernels (below)
+// for 32-wide ones
 IC2_HG4_KERNEL(hg4_o128_w16_s4_kernel, 8, 4, 1, 4, 16, 4)  // 128 o x (16 x 16) px
 IC2_HG4_KERNEL(hg4_o192_w16_s4_kernel, 6, 4, 2, 2, 16, 4)  // 192 o x (8 x 16) px
 IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)   // 64 o x (16 x 16) px
-IC2_HG4_KERNEL_HB(hg4_o128_w32_hb_kernel, 8, 4, 1, 4, 32, 4)  // 128 o x (8 x 32) px
-IC2_HG4_KERNEL_HB(hg4_o192_w32_hb_kernel, 6, 4, 2, 2, 32, 4)  // 192 o x (4 x 32) px
-IC2_HG4_KERNEL_HB(hg4_o64_w32_hb_kernel, 4, 4, 1, 4, 32, 4)   // 64 o x (8 x 32) px
+#define IC2_HG4_KERNEL_P(name, I, J, WGO, WGP, TW, NS, TPB)                                                     \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name(IgemmArgs a, int tx,  \
+                                                                                          int ty) {            \
+    hg4_body<I, J, WGO, WGP, TW, NS, true, false, TPB>(a, tx, ty);                                               \
+  }                                                                                                              \
+  __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) name##_f16(IgemmArgs a,     \
+                                                                                                int tx, int ty) { \
+    hg4_body<I, J, WGO, WGP, TW, NS, true, true, TPB>(a, tx, ty);                                                \
+  }
+// 32-wide tiles: halo burst + several taps per barrier (two for o128 / o192, whose 4-slab ring and double halo
+// fill the 80 KB; three for o64 with a 6-slab ring, one barrier per kernel row), profiles/r3_hg4_taps_ab.txt
+IC2_HG4_KERNEL_P(hg4_o128_w32_p2_kernel, 8, 4, 1, 4, 32, 4, 2)  // 128 o x (8 x 32) px
+IC2_HG4_KERNEL_P(hg4_o192_w32_p2_kernel, 6, 4, 2, 2, 32, 4, 2)  // 192 o x (4 x 32) px
+IC2_HG4_KERNEL_P(hg4_o64_w32_p3_kernel, 4, 4, 1, 4, 32, 6, 3)   // 64 o x (8 x 32) px
 #undef IC2_HG4_KERNEL
-#undef IC2_HG4_KERNEL_HB
+#undef IC2_HG4_KERNEL_P
 
 // instance: o-tile 192 when cout_p % 192 == 0, 128 when cout_p % 128 == 0, else 64 (IC2_HG4_BO=128 forces 128 where
 // it divides); pixel tile 32 or 16 wide, whichever pads the output less
@@ -961,9 +1023,9 @@ static void launch_hg4(IgemmArgs a, hipStream_t s, void (*kern)(IgemmArgs, int, 
 static void hg4_dispatch(const IgemmArgs& a, hipStream_t s, bool f16) {
   const H4Plan p = h4_plan(a.n, a.ho, a.wo, a.cout_p);
   if (p.tw32) {
-    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, f16 ? hg4_o192_w32_hb_kernel_f16 : hg4_o192_w32_hb_kernel);
-    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, f16 ? hg4_o128_w32_hb_kernel_f16 : hg4_o128_w32_hb_kernel);
-    else launch_hg4<4, 4, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_hb_kernel_f16 : hg4_o64_w32_hb_kernel);
+    if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, f16 ? hg4_o192_w32_p2_kernel_f16 : hg4_o192_w32_p2_kernel);
+    else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, f16 ? hg4_o128_w32_p2_kernel_f16 : hg4_o128_w32_p2_kernel);
+    else launch_hg4<4, 4, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_p3_kernel_f16 : hg4_o64_w32_p3_kernel);
   } else {
     if (p.bo == 192) launch_hg4<6, 4, 2, 2, 16>(a, s, f16 ? hg4_o192_w16_s4_kernel_f16 : hg4_o192_w16_s4_kernel);
     else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 16>(a, s, f16 ? hg4_o128_w16_s4_kernel_f16 : hg4_o128_w16_s4_kernel);
@@ -1470,7 +1532,7 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
       return buf;
     case CK_HG4: {
       const H4Plan p = h4_plan(n, ho, wo, cout_p);
-      snprintf(buf, sizeof(buf), "hg4_o%d_w%s", p.bo, p.tw32 ? "32_hb" : "16_s4");
+      snprintf(buf, sizeof(buf), "hg4_o%d_w%s", p.bo, !p.tw32 ? "16_s4" : p.bo == 64 ? "32_p3" : "32_p2");
       return buf;
     }
     default: break;

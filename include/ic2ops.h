@@ -157,7 +157,7 @@ int ic2_modconv_prep_batched(const float* ws, int64_t ldx, int n, int w_dim, int
                              void* stream);
 
 /* The kernel instance(s) ic2_conv_igemm_ws launches for a geometry (its launch plan; host-only, no GPU needed),
- * e.g. "igemm8_og2", "hg4_o128_w32_hb", "hconv_64_64", "torgb", "igemm_128x128_splitk".  Static storage. */
+ * e.g. "igemm8_og2", "hg4_o128_w32_p2", "hconv_64_64", "torgb", "igemm_128x128_splitk".  Static storage. */
 const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, int n, int h, int w, int cin_p, int cout_p,
                           int cout_valid, int kh, int kw, int pad);
 
