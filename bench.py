@@ -157,6 +157,8 @@ def conv_call_plan(nv, name, args):
     elif name == "ic2_conv3x3_gn_fwd":
         dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[3], args[4:13]
         odt, layout = dt, nv.NHWC
+        if dt == nv.BF16X3:  # split-bf16 encoder: bf16 GEMM over the tripled K, f32 out
+            dt, odt = nv.BF16, nv.F32
     elif name == "ic2_conv3x3_gnin_gn_fwd":
         dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[5], args[6:15]
         odt, layout = dt, nv.NHWC

@@ -499,6 +499,8 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
                   int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
                   const float* in_gn, float in_slope);
 bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad);
+bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                   int groups, int fuse_mode);
 int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
                                    int groups);
 
@@ -755,12 +757,18 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
                                 (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope);
   if (nch == -2) return IC2_E_UNSUPPORTED;
   if (nch < 0) return IC2_E_INVALID;
-  if (nch == 0)
-    return ic2_group_norm_stats(y, dtype, n, ho * wo, cout_p, cout_valid, groups, eps, stats, stream);
+  if (nch == 0)  // split-bf16 input: the conv wrote f32
+    return ic2_group_norm_stats(y, dtype == IC2_BF16X3 ? IC2_F32 : dtype, n, ho * wo, cout_p, cout_valid, groups, eps,
+                                stats, stream);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups, nch,
                      (double)ho * wo * (cout_valid / groups), eps, stats);
   IC2_CHECK_LAUNCH("conv3x3_gn_fwd");
   return IC2_OK;
+}
+
+extern "C" int ic2_conv3x3_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh,
+                                    int kw, int pad, int groups, int fuse) {
+  return conv_gn_fuses(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, fuse) ? 1 : 0;
 }
 
 extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,

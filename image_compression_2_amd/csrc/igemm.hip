@@ -108,7 +108,7 @@ __device__ __forceinline__ void ig_preloads_done() { __builtin_amdgcn_s_waitcnt(
 // stored NHWC / NHWC16 (bf16 / f16 / f32) or NCHW (f32, channels < cout_valid only); sc / bi = the preloaded
 // oscale[nn][ob..ob+3] / bias[ob..ob+3].
 __device__ __forceinline__ void ig_store4v(const IgemmArgs& a, int p, int nn, int pix, int ob, const float (&acc)[4],
-                                           float4 sc, float4 bi) {
+                                           float4 sc, float4 bi, float (*vout)[4] = nullptr) {
   const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, biv[4] = {bi.x, bi.y, bi.z, bi.w};
   float v[4];
 #pragma unroll
@@ -116,6 +116,10 @@ __device__ __forceinline__ void ig_store4v(const IgemmArgs& a, int p, int nn, in
     float t = acc[r] * scv[r] + biv[r];
     if (a.act) t = lrelu_gain_clamp(t, a.slope, a.act_gain, a.clamp);
     v[r] = t * a.out_mul;
+  }
+  if (vout != nullptr) {  // the f32 values this call stores (the fused GroupNorm statistics read them)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) (*vout)[r] = v[r];
   }
   if (a.out_layout != IC2_LAYOUT_NCHW) {
     // NHWC, or channel-blocked NHWC16 [n][cout_p / 16][ho][wo][16] (the fused filtered lrelu's input: its
@@ -729,7 +733,8 @@ __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((
 // HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
 // past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
 // chain, ~60 SALU per step) and a wait count that depends only on the tap
-template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false, int TPB = 1>
+template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false, int TPB = 1,
+          bool GN = false>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = H4<I, J, WGO, WGP, TW, NS, HB>;
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
@@ -939,6 +944,15 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     bi[i] = ig_load_bias(a, o0 + obase + i * 16 + 4 * fh);
   }
   ig_preloads_done();
+  // GN: 32 groups over cout_p = BO channels; a lane's 4 channels of block i are GL whole groups of CPG
+  constexpr int CPG = G::BO / 32, GL = 4 / CPG;
+  float gs[GN ? I : 1][GL], gq[GN ? I : 1][GL];  // per-group sums of the stored values over this lane's pixels
+  if constexpr (GN) {
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int r = 0; r < GL; ++r) gs[i][r] = gq[i][r] = 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int pb = pg * J + j;
@@ -951,7 +965,55 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
       const int ob = o0 + obase + i * 16 + 4 * fh;
       if (ob >= a.cout_p) continue;
       const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
+      if constexpr (GN) {
+        float st[4];
+        ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i], &st);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gs[i][r / CPG] += st[r];
+          gq[i][r / CPG] += st[r] * st[r];
+        }
+      } else {
+        ig_store4v(a, p, nn, pix, ob, v, sc[i], bi[i]);
+      }
+    }
+  }
+  if constexpr (GN) {
+    // GroupNorm partial sums of this tile: the 16 pixel lanes by an xor tree, the WGP pixel waves of a channel
+    // block through LDS, then one thread per group adds the waves in a fixed order in f64 -> gn_part[(nn, g, tile)]
+    static_assert(G::BO == 64 || G::BO == 128, "GN epilogue: 2 or 4 channels per group");
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int r = 0; r < GL; ++r)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          gs[i][r] += __shfl_xor(gs[i][r], off, 64);
+          gq[i][r] += __shfl_xor(gq[i][r], off, 64);
+        }
+    __syncthreads();  // every wave is past its last LDS fragment read
+    float* red = reinterpret_cast<float*>(lds);  // [2][WGP][32 groups]
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int r = 0; r < GL; ++r) {
+          const int g = (obase + i * 16 + 4 * fh) / CPG + r;
+          red[pg * 32 + g] = gs[i][r];
+          red[(WGP + pg) * 32 + g] = gq[i][r];
+        }
+    }
+    __syncthreads();
+    if (tid < 32) {
+      double sg = 0.0, qg = 0.0;
+#pragma unroll
+      for (int w = 0; w < WGP; ++w) {
+        sg += (double)red[w * 32 + tid];
+        qg += (double)red[(WGP + w) * 32 + tid];
+      }
+      double* o = a.gn_part + (((int64_t)nn * 32 + tid) * (tiles_x * tiles_y) + (ty * tiles_x + tx)) * 2;
+      o[0] = sg;
+      o[1] = qg;
     }
   }
 }
@@ -984,6 +1046,15 @@ IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)   // 64 o x (16 x 16) p
 IC2_HG4_KERNEL_P(hg4_o128_w32_p2_kernel, 8, 4, 1, 4, 32, 4, 2)  // 128 o x (8 x 32) px
 IC2_HG4_KERNEL_P(hg4_o192_w32_p2_kernel, 6, 4, 2, 2, 32, 4, 2)  // 192 o x (4 x 32) px
 IC2_HG4_KERNEL_P(hg4_o64_w32_p3_kernel, 4, 4, 1, 4, 32, 6, 3)   // 64 o x (8 x 32) px
+// the split-bf16 encoder's 64- / 128-wide convs with the GroupNorm statistics of their f32 output in the epilogue
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o64_w32_p3_gn_kernel(IgemmArgs a, int tx, int ty) {
+  hg4_body<4, 4, 1, 4, 32, 6, true, false, 3, true>(a, tx, ty);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o128_w32_p2_gn_kernel(IgemmArgs a, int tx, int ty) {
+  hg4_body<8, 4, 1, 4, 32, 4, true, false, 2, true>(a, tx, ty);
+}
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_P
 
@@ -1679,12 +1750,78 @@ bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p
   return hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw);
 }
 
+// split-bf16 (IC2_BF16X3) conv with f32 output: the hg4 instance the plan picks carries the statistics in its
+// epilogue when it is a 32-wide-tile o64 / o128 kernel over exactly 32 groups of 2 / 4 channels
+static bool x3_gn_hg4(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int groups,
+                      H4Plan* plan) {
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (ho <= 0 || wo <= 0 || groups != 32 || cout_valid != cout_p || (cout_p != 64 && cout_p != 128)) return false;
+  const ConvChoice c = conv_choice(IC2_BF16, IC2_LAYOUT_NHWC, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  if (c.kind != CK_HG4) return false;
+  const H4Plan p = h4_plan(n, ho, wo, cout_p);
+  if (!p.tw32 || p.bo != cout_p) return false;
+  if (plan) *plan = p;
+  return true;
+}
+
+static int64_t x3_gn_part_doubles(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                                  int groups) {
+  if (!x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr)) return 0;
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, 8) * 2;  // o64 / o128 w32 tiles: 8 x 32 pixels
+}
+
+bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                   int groups, int fuse_mode) {
+  static const bool x3_env = knob("IC2_X3_GN", 1) == 1;  // A/B: 0 = the separate statistics pass by default
+  if (dtype == IC2_BF16X3)
+    return (fuse_mode > 0 || (fuse_mode < 0 && x3_env)) &&
+           x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr);
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  if (ho <= 0 || wo <= 0) return false;
+  static const bool fuse_env = knob("IC2_CONV_GN", 0) == 1;
+  const bool fuse_req = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
+  return fuse_req && hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw) && groups == 32 &&
+         cout_valid == cout_p;
+}
+
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                   int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
                   int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
                   const float* in_gn, float in_slope) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
+  if (dtype == IC2_BF16X3) {
+    // default on: the statistics epilogue of the non-persistent hg4 costs less than the separate f32 pass saves
+    H4Plan p;
+    const bool fuse = conv_gn_fuses(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, fuse_mode) &&
+                      in_gn == nullptr && bias != nullptr && part != nullptr &&
+                      x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, &p) &&
+                      part_doubles >= x3_gn_part_doubles(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups);
+    if (in_gn != nullptr) {
+      set_error("conv3x3_gnin_gn_fwd: no input GroupNorm fusion in split-bf16 mode");
+      return -2;
+    }
+    if (!fuse) {
+      const int rc = ic2_conv_igemm_ws(x, w, y, IC2_BF16, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
+                                       ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace,
+                                       ws_bytes, s);
+      return rc == IC2_OK ? 0 : -1;
+    }
+    IgemmArgs a;
+    a.x = x; a.w = w; a.y = y; a.oscale = nullptr; a.bias = bias; a.ws = nullptr;
+    a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
+    a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
+    a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
+    a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = 1.f;
+    a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = IC2_F32;
+    a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
+    a.group = 1; a.korder = 0; a.o_base = 0;
+    a.in_gn = nullptr; a.in_slope = 0.f;
+    if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
+    else launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_p2_gn_kernel);
+    return (int)(ceil_div(wo, 32) * ceil_div(ho, 8));
+  }
   const bool hconv = hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
   const int th = cin_p > 64 ? 4 : 8;
   const int64_t nch = ceil_div(wo, 32) * ceil_div(ho, th);
@@ -1735,6 +1872,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
 
 int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
                                    int groups) {
+  if (dtype == IC2_BF16X3) return x3_gn_part_doubles(n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad, groups);
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (!hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw)) return 0;
   const int th = cin_p > 64 ? 4 : 8;

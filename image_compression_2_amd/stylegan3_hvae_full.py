@@ -154,6 +154,18 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     wp, bp = _packed(conv, x, dt, cache, stream)
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
+    if x.x3 and bool(nv.query("ic2_conv3x3_gn_fuses", nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw, pad,
+                              norm.num_groups, int(fuse))):
+        # split bf16, 64- / 128-wide layers: the 4-wave halo GEMM writes f32 and the statistics in one launch
+        y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
+        nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, kh, kw, pad,
+                           norm.num_groups))
+        stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
+        nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
+        nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, cout,
+                kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, None, 0, int(fuse),
+                stream)
+        return _Act(y, cout), stats
     if x.x3:
         # split bf16: one bf16 implicit GEMM over the tripled K, f32 out, GroupNorm statistics on the f32 values
         y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)

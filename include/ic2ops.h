@@ -303,12 +303,18 @@ int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_
  * ic2_group_norm_stats runs after the conv.  stats: ic2_conv3x3_gn_stats_floats() floats (statistics + partial
  * sums); conv_ws / conv_ws_bytes: the conv's split-K workspace as for ic2_conv_igemm_ws.  fuse: 1 = fused statistics
  * where the halo conv runs, 0 = always the separate pass, -1 = default (separate; env IC2_CONV_GN=1 fuses -- measured
- * at parity on MI355X).  Deterministic. */
+ * at parity on MI355X).  Deterministic.  dtype IC2_BF16X3: the split-bf16 encoder -- x bf16 with
+ * cin_p = the tripled channel count ([hi | hi | lo]), w from ic2_pack_weight(IC2_BF16X3), y f32 NHWC; the
+ * statistics come out of the 4-wave halo GEMM's epilogue (on the f32 values as stored) when it runs a 64- / 128-wide
+ * layer with 32 groups (fuse != 0), else the separate pass. */
 int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad,
                                     int groups);
 int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                        int cout_valid, int kh, int kw, int pad, const float* bias, int groups, float eps, float* stats,
                        int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse, void* stream);
+/* 1 when ic2_conv3x3_gn_fwd with these arguments takes the statistics from the conv's epilogue (a host query). */
+int ic2_conv3x3_gn_fuses(int dtype, int n, int h, int w, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                         int groups, int fuse);
 
 /* VGGBlock's second conv with the first GroupNorm + lrelu applied to its INPUT as the halo conv stages it
  * (stylegan3_hvae_full.py:183-191: conv2(lrelu(norm1(conv1(x))))): the normalised activation is never written to
