@@ -1750,15 +1750,19 @@ bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p
   return hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw);
 }
 
-// split-bf16 (IC2_BF16X3) conv with f32 output: the hg4 instance the plan picks carries the statistics in its
-// epilogue when it is a 32-wide-tile o64 / o128 kernel over exactly 32 groups of 2 / 4 channels
+static int conv_chunk_n(int dtype, int n, int h, int w_, int cin_p);
+
+// split-bf16 (IC2_BF16X3) conv with f32 output: the hg4 instance the plan picks (per chunk of images, as
+// ic2_conv_igemm_ws launches it) carries the statistics in its epilogue when it is a 32-wide-tile o64 / o128 kernel
+// over exactly 32 groups of 2 / 4 channels
 static bool x3_gn_hg4(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int groups,
                       H4Plan* plan) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (ho <= 0 || wo <= 0 || groups != 32 || cout_valid != cout_p || (cout_p != 64 && cout_p != 128)) return false;
-  const ConvChoice c = conv_choice(IC2_BF16, IC2_LAYOUT_NHWC, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  const int nc = conv_chunk_n(IC2_BF16, n, h, w_, cin_p);
+  const ConvChoice c = conv_choice(IC2_BF16, IC2_LAYOUT_NHWC, IC2_F32, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
   if (c.kind != CK_HG4) return false;
-  const H4Plan p = h4_plan(n, ho, wo, cout_p);
+  const H4Plan p = h4_plan(nc, ho, wo, cout_p);
   if (!p.tw32 || p.bo != cout_p) return false;
   if (plan) *plan = p;
   return true;
@@ -1818,9 +1822,19 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;
     a.in_gn = nullptr; a.in_slope = 0.f;
-    if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
-    else launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_p2_gn_kernel);
-    return (int)(ceil_div(wo, 32) * ceil_div(ho, 8));
+    const int nc = conv_chunk_n(IC2_BF16, n, h, w_, cin_p);
+    const int64_t ntile = ceil_div(wo, 32) * ceil_div(ho, 8);
+    for (int i0 = 0; i0 < n; i0 += nc) {  // chunks of whole images (< 2^31 input bytes per launch)
+      const int cnt = n - i0 < nc ? n - i0 : nc;
+      a.x = reinterpret_cast<const char*>(x) + (int64_t)i0 * h * w_ * cin_p * 2;
+      a.y = reinterpret_cast<char*>(y) + (int64_t)i0 * ho * wo * cout_p * 4;
+      a.gn_part = part + (int64_t)i0 * groups * ntile * 2;
+      a.n = cnt;
+      a.M = (int)((int64_t)cnt * ho * wo);
+      if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
+      else launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_p2_gn_kernel);
+    }
+    return (int)ntile;
   }
   const bool hconv = hconv_eligible(dtype, M, cin_p, cout_p, kh, kw);
   const int th = cin_p > 64 ? 4 : 8;
