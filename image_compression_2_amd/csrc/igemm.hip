@@ -544,7 +544,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 #define IC2_G8_ISSUE_A(h_, buf_, c_)                                                                          \
   {                                                                                                          \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(                                     \
-        (void*)(wg + (int64_t)(((c_).ky * a.kw + (c_).kx) * CB + (c_).cb) * 128), 0, (c_).t < a.nq ? kOob : 0,  \
+        (void*)(wg + (int64_t)(((c_).ky * a.kw + (c_).kx) * CB + (c_).cb) * 128), 0, (c_).t < t_end ? kOob : 0, \
         kRsrcWord3);                                                                                         \
     _Pragma("unroll") for (int k = 0; k < NA; ++k)                                                           \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G::BUF + \
@@ -556,7 +556,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
     const int tap = (c_).ky * a.kw + (c_).kx;                                                                \
     const int64_t sh = ((int64_t)((c_).ky - a.pad) * a.w_ + ((c_).kx - a.pad)) * a.cin_p * 2 + (c_).cb * 128;  \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(xg + sh), 0,                  \
-                                                                        (c_).t < a.nq ? kOob : 0, kRsrcWord3); \
+                                                                        (c_).t < t_end ? kOob : 0, kRsrcWord3); \
     _Pragma("unroll") for (int k = 0; k < NB; ++k) {                                                         \
       const uint32_t vo = ((x_tap[h_][k] >> tap) & 1u) ? x_off[h_][k] : kOob;                                \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (buf_) * G::BUF + \
@@ -577,8 +577,22 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   const int orow = o0 + grp * 128;
   const bool live0 = orow < a.cout_p, live1 = orow + 64 < a.cout_p;
 
+  // split-K (gridDim.y slices, small grids): this workgroup's K-tiles [t_begin, t_end); tiles past t_end come in
+  // as zeros (descriptor size 0), so the phase loop needs no tail case
+  const int per = (a.nq + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int t_begin = __builtin_amdgcn_readfirstlane(min(a.nq, (int)blockIdx.y * per));
+  const int t_end = __builtin_amdgcn_readfirstlane(min(a.nq, t_begin + per));
+  const int ntap = a.kh * a.kw;
+  Cur c0;
+  c0.t = t_begin;
+  {
+    const int tap = cmaj ? t_begin % ntap : t_begin / CB;
+    c0.cb = __builtin_amdgcn_readfirstlane(cmaj ? t_begin / ntap : t_begin % CB);
+    c0.ky = __builtin_amdgcn_readfirstlane(tap / a.kw);
+    c0.kx = __builtin_amdgcn_readfirstlane(tap - (tap / a.kw) * a.kw);
+  }
+
   // prologue: tile 0 -> buf0 (all four halves), tile 1 -> buf1.A0 / buf1.B1 (what phases 6-7 would issue)
-  Cur c0{0, 0, 0, 0};
   Cur c1 = advance(c0);
   IC2_G8_ISSUE_A(0, 0, c0);
   IC2_G8_ISSUE_B(0, 0, c0);
@@ -617,7 +631,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 #define IC2_G8_NOWAIT (void)0
 #define IC2_G8_WAIT asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory")
 
-  const int niter = (a.nq + 1) >> 1;
+  const int niter = (t_end - t_begin + 1) >> 1;
   Cur cn = c1;  // tile 2i+1
   for (int it = 0; it < niter; ++it) {
     const Cur cA = cn;               // 2i+1
@@ -686,15 +700,15 @@ static void launch_igemm(IgemmArgs a, int splits, hipStream_t s) {
 }
 
 template <int OG, bool F16 = false>
-static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1) {
+static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1, int splits = 1) {
   a.o_base = o_base;
   a.tiles_o = ((o_end < 0 ? a.cout_p : o_end) - o_base + G8<OG>::BO - 1) / G8<OG>::BO;
   a.nq = a.K / 64;
   a.nblocks = (int)(ceil_div(a.M, G8<OG>::BP) * a.tiles_o);
   if constexpr (OG == 2)
-    hipLaunchKernelGGL(F16 ? igemm8_og2_f16_kernel : igemm8_og2_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(F16 ? igemm8_og2_f16_kernel : igemm8_og2_kernel, dim3(a.nblocks, splits), dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL(F16 ? igemm8_og1_f16_kernel : igemm8_og1_kernel, dim3(a.nblocks), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(F16 ? igemm8_og1_f16_kernel : igemm8_og1_kernel, dim3(a.nblocks, splits), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1157,11 +1171,24 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && x_elems * 2 < (int64_t)kOob &&
                        (int64_t)cout_p * K * 2 < (int64_t)kOob;
     const bool odd128 = cout_p % 256 == 128 && cout_p > 128;
-    if (fits8 && cout_p > 128 && !odd128 && ceil_div(M, 256) * ((cout_p + 255) / 256) >= 240) tile = 6;
-    else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) &&
-             ceil_div(M, 512) * ((cout_p + 127) / 128) >= 240) tile = 7;
-    if (forced >= 1 && forced <= 7) tile = forced;
-    if ((tile == 6 || tile == 7) && !fits8) tile = 1;
+    // small grids (the encoder's 512-wide blocks at <= 32^2): the same 8-phase tiles with K split over
+    // gridDim.y so the launch reaches ~1 workgroup per CU, instead of the 4-stage 128 x 128 split-K tile
+    static const bool g8_splitk = knob("IC2_G8_SPLITK", 1) != 0;
+    const int64_t g6 = ceil_div(M, 256) * ((cout_p + 255) / 256), g7 = ceil_div(M, 512) * ((cout_p + 127) / 128);
+    const bool k_deep = K / 64 >= 32;
+    int g8_split = 1;
+    if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) tile = 6;
+    else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) && g7 >= 240) tile = 7;
+    else if (g8_splitk && splitk && fits8 && k_deep && cout_p > 128 && !odd128) tile = 6, g8_split = (int)ceil_div(240, g6);
+    if (g8_split > 1) {
+      int64_t sp = g8_split;
+      if (sp > K / 64 / 8) sp = K / 64 / 8;  // >= 8 K-tiles of 64 per slice
+      if (sp > 32) sp = 32;
+      g8_split = M * cout_p < (1LL << 31) ? (int)sp : 1;
+    }
+    if (forced >= 1 && forced <= 7) tile = forced, g8_split = 1;
+    if ((tile == 6 || tile == 7) && !fits8) tile = 1, g8_split = 1;
+    if (g8_split > 1) return IgPlan{tile, BOs[tile], BPs[tile], g8_split};
   }
   IgPlan pl{tile, BOs[tile], BPs[tile], 1};
   if (tile < 6 && splitk) {
@@ -1523,13 +1550,13 @@ static void launch_torgb(const IgemmArgs& a, hipStream_t s) {
 template <bool F16>
 static void launch_igemm16(const IgemmArgs& a, hipStream_t s, const IgPlan& pl, bool split384, int cout_p) {
   switch (pl.tile) {
-    case 6: launch_g8<2, F16>(a, s); break;
+    case 6: launch_g8<2, F16>(a, s, 0, -1, pl.splits); break;
     case 7:
       if (split384) {
-        launch_g8<2, F16>(a, s, 0, cout_p - 128);
-        launch_g8<1, F16>(a, s, cout_p - 128, cout_p);
+        launch_g8<2, F16>(a, s, 0, cout_p - 128, pl.splits);
+        launch_g8<1, F16>(a, s, cout_p - 128, cout_p, pl.splits);
       } else {
-        launch_g8<1, F16>(a, s);
+        launch_g8<1, F16>(a, s, 0, -1, pl.splits);
       }
       break;
     case 1: launch_igemm<true, 256, 256, 2, 4, 4, F16>(a, pl.splits, s); break;
@@ -1612,7 +1639,7 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
     snprintf(buf, sizeof(buf), "igemm_f32_128x128%s", c.pl.splits > 1 ? "_splitk" : "");
     return buf;
   }
-  if (c.pl.tile == 6) return "igemm8_og2";
+  if (c.pl.tile == 6) return c.pl.splits > 1 ? "igemm8_og2_splitk" : "igemm8_og2";
   if (c.pl.tile == 7) return c.split384 ? "igemm8_og2+og1" : "igemm8_og1";
   snprintf(buf, sizeof(buf), "igemm_%dx%d%s", c.pl.bo, c.pl.bp, c.pl.splits > 1 ? "_splitk" : "");
   return buf;

@@ -398,6 +398,20 @@ def test_conv_halo_gemm4(cuda, cin, cout, size, pad, dtype):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("cin,cout,size,pad,n", [(512, 512, 12, 1, 3), (1024, 320, 9, 1, 2), (768, 256, 7, 2, 5),
+                                                 (512, 512, 2, 1, 8)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_g8_splitk(cuda, cin, cout, size, pad, n, dtype):
+    """Small grids of the 8-phase 256 x 256 kernel split K over gridDim.y (slices of >= 8 K-tiles, zero tiles past a
+    slice's end, the split-K combine): the plan picks it on these shapes (partial o-tiles: 320; 2 x 2 images) and
+    the result matches F.conv2d in fp64."""
+    ho = size + 2 * pad - 2
+    dc = nv.F16 if dtype == torch.float16 else nv.BF16
+    assert nv.conv_plan(dc, dc, nv.NHWC, n, size, size, cin, nv.pad32(cout), cout, 3, 3, pad).startswith(
+        "igemm8_og2_splitk"), (cin, cout, size, ho)
+    _conv_case(cin, cout, size, pad, dtype, n=n)
+
+
 @pytest.mark.parametrize("cin,cout,size,pad", [(128, 362, 88, 2), (96, 384, 81, 1)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_split_384(cuda, cin, cout, size, pad, dtype):
