@@ -1118,7 +1118,7 @@ static void hg4_dispatch(const IgemmArgs& a, hipStream_t s, bool f16) {
   }
 }
 
-// bf16 3x3 with 32-deep channel blocks.  Default: on a grid of >= 2 workgroups per CU, <= 256 channels in, <= 192
+// bf16 3x3 with 32-deep channel blocks.  Default: on a grid of >= 2 workgroups per CU, <= 512 channels in, <= 192
 // out, >= 93 % pixel-tile utilisation (tools/sweep_igemm.py, profiles/r2e_hg4_sweep.txt).  Knob IC2_HG4 (IC2_DEV=1):
 // 0 disables it, 2 forces it wherever legal (the tests' forced-instance runs).
 static bool hg4_legal(int dtype, int cin_p, int cout_p, int kh, int kw, int64_t x_elems) {
@@ -1133,7 +1133,10 @@ static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64
   if (p.blocks < 512) return false;
   const int th = (p.bo <= 128 ? 256 : 128) / (p.tw32 ? 32 : 16);
   const double util = (double)ho * wo / ((double)ceil_div(ho, th) * th * ceil_div(wo, p.tw32 ? 32 : 16) * (p.tw32 ? 32 : 16));
-  return cin_p <= 256 && cout_p <= 192 && util >= 0.93;
+  // inputs up to 512 channels (the split encoder's 384-wide block-1 conv2: og1 -> hg4 + fused statistics, C4
+  // +1.1 %, profiles/r3_hg4_maxc_ab.txt); knob IC2_HG4_MAXC for the A/B
+  static const int maxc = knob("IC2_HG4_MAXC", 512);
+  return cin_p <= maxc && cout_p <= 192 && util >= 0.93;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -383,7 +383,8 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad, dtype):
 
 @pytest.mark.parametrize("cin,cout,size,pad", [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1),
                                               (256, 256, 30, 2), (32, 256, 29, 1), (128, 384, 20, 1), (64, 320, 21, 1),
-                                              (181, 128, 37, 2), (81, 51, 37, 2), (64, 64, 33, 1)])
+                                              (181, 128, 37, 2), (81, 51, 37, 2), (64, 64, 33, 1), (384, 128, 24, 1),
+                                              (512, 192, 21, 1)])
 @pytest.mark.parametrize("dtype", ["torch.bfloat16", "torch.float16"])
 def test_conv_halo_gemm4(cuda, cin, cout, size, pad, dtype):
     """The 4-wave halo implicit GEMM (hg4: 32-channel blocks, two workgroups per CU) forced on every instance
