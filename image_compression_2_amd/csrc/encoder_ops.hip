@@ -747,6 +747,10 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
                                int fuse, void* stream, const float* in_gn, float in_slope) {
   IC2_CHECK_ARG(x && w && y && stats && groups > 0 && cout_valid > 0 && cout_valid % groups == 0,
                 "conv3x3_gn_fwd: bad arguments");
+  // the encoder's precisions only: the fused statistics epilogue and the input-GroupNorm staging are bf16 halo-conv
+  // code, and an f16 operand must never reach the bf16 MFMA
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_BF16X3,
+                "conv3x3_gn_fwd: dtype must be IC2_F32, IC2_BF16 or IC2_BF16X3");
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   IC2_CHECK_ARG(stats_floats >= ic2_conv3x3_gn_stats_floats(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad, groups),
                 "conv3x3_gn_fwd: stats buffer too small");

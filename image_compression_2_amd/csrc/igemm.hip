@@ -1815,8 +1815,9 @@ bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int c
   if (ho <= 0 || wo <= 0) return false;
   static const bool fuse_env = knob("IC2_CONV_GN", 0) == 1;
   const bool fuse_req = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
-  return fuse_req && hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw) && groups == 32 &&
-         cout_valid == cout_p;
+  // the statistics epilogue exists for the bf16 halo conv only (hconv_eligible also admits f16 operands)
+  return fuse_req && dtype == IC2_BF16 && hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw) &&
+         groups == 32 && cout_valid == cout_p;
 }
 
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
@@ -1875,7 +1876,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   // r2b_conv_gn_ab.txt); knob IC2_CONV_GN=1 enables it.
   static const bool fuse_env = knob("IC2_CONV_GN", 0) == 1;
   const bool fuse_req = fuse_mode < 0 ? fuse_env : fuse_mode > 0;
-  const bool fuse = fuse_req && hconv && part != nullptr && part_doubles >= (int64_t)n * groups * nch * 2 &&
+  const bool fuse = fuse_req && hconv && dtype == IC2_BF16 && part != nullptr && part_doubles >= (int64_t)n * groups * nch * 2 &&
                     groups == 32 && cout_valid == cout_p && bias != nullptr;
   if (in_gn != nullptr && !conv_gn_in_supported(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad)) {
     set_error("conv3x3_gn_fwd: input GroupNorm fusion needs the halo conv (bf16, cin_p 64)");
@@ -1918,7 +1919,7 @@ int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, i
                                    int groups) {
   if (dtype == IC2_BF16X3) return x3_gn_part_doubles(n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad, groups);
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
-  if (!hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw)) return 0;
+  if (dtype != IC2_BF16 || !hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw)) return 0;
   const int th = cin_p > 64 ? 4 : 8;
   return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, th) * 2;
 }

@@ -385,6 +385,17 @@ class SynthesisLayer(torch.nn.Module):
                           nv.ACT_LRELU, 1.0, 1.0, clamp, float(1.0 if final_scale is None else final_scale), nv.NCHW,
                           stream, x.device)
             return out
+        y, blocked = self.conv_nhwc(x, n, dt, oscale)
+        return self.flrelu_nhwc(y, dt, post_scale, blocked=blocked)
+
+    def conv_nhwc(self, x, n, dt, oscale):
+        """The modulated conv of a non-ToRGB layer: -> (conv output y, blocked layout?) for flrelu_nhwc."""
+        s_in = int(self.in_size[0])
+        k = self.conv_kernel
+        pad = k - 1
+        conv = s_in + 2 * pad - k + 1
+        wp, _, bp = self.packed(dt)
+        stream = nv.stream_of(x)
         # bf16 / f16 mode: the conv output feeds the MFMA filtered-lrelu, whose operands are f16 -> store it as f16, in
         # the channel-blocked layout [n][cout_p/16][conv][conv][16] the fused kernel's 16-channel tiles read as
         # contiguous rows (IC2_FLR_BLOCKED=0: plain NHWC)
@@ -397,7 +408,7 @@ class SynthesisLayer(torch.nn.Module):
         nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
                       self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
                       0.0, 1.0, -1.0, 1.0, nv.NHWC16 if blocked else nv.NHWC, stream, x.device)
-        return self.flrelu_nhwc(y, dt, post_scale, blocked=blocked)
+        return y, blocked
 
     def flrelu_nhwc(self, y, dt_out, post_scale=None, blocked=False):
         """The layer's filtered lrelu on the conv output y NHWC [n, conv, conv, cout_p] (f32, or f16 for the

@@ -9,6 +9,15 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def golden_script(name):
+    """A fixture-generating script under tests/golden/ as a module (its input builders are what the tests feed)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(f"golden_{name}", os.path.join(GOLDEN, name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built libic2ops.so")
 

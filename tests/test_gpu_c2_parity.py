@@ -1,11 +1,13 @@
 """Parity of the BENCHED mode: the exact C2 workload (BASELINE.json configs[1]) -- batch 32, 256^2,
-HVAE_VGG_Encoder(img_resolution=1024) -> 8-bit uniform quantizer -> SG3-T-256 synthesis, in bench.py's default
-precisions (encoder split-bf16 'bf16x3', synthesis bf16) -- against the oracle.
+HVAE_VGG_Encoder(img_resolution=1024) -> 8-bit uniform quantizer -> SG3-T-256 synthesis, in bench.py's precisions
+(encoder split-bf16 'bf16x3'; synthesis f16 = the default since round 4, and bf16) -- against the oracle.
 
 Reference path: stylegan3_hvae_full.py:295-329 (compress -> decompress), metric hvae_training.py:368-395.
-The fp32 oracle means come from oracle/encoder.py (pinned to the reference's own encoder by
-tests/golden/encoder_full.npz); the reference reconstruction is the fp32 path on the oracle's quantized
-latents (pinned to the CPU synthesis restatement at 1e-3 by test_gpu_path.py, re-checked here on 2 images).
+The fp32 oracle means of this exact input (bench.py's rank-0 batch) are the committed fixture
+tests/golden/parity_means.npz (tests/golden/make_parity_means.py: oracle/encoder.py, pinned to the reference's own
+encoder by tests/golden/encoder_full.npz; the fixture itself is re-derived on 2 images by
+tests/test_oracle.py::test_parity_means_fixture); the reference reconstruction is the fp32 path on the oracle's
+quantized latents (pinned to the CPU synthesis restatement at 1e-3 by test_gpu_path.py, re-checked here on 1 image).
 
 What is asserted (thresholds are module constants, measured values are printed and recorded in DESIGN.md (c)):
   (a) quantized indices (north star: bit-exact): the benched encoder's means within ENC_TOL of the oracle's;
@@ -22,6 +24,9 @@ floor and against the PSNR bar at both operating points, 46 dB included.
 The perturbation test shows (b) can fail: one bf16-ulp (2^-8) error in every layer's filtered-lrelu gain
 or up-filter taps drops the SNR below the floor.
 """
+import hashlib
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -32,6 +37,7 @@ from oracle import encoder as oe
 from oracle import sg3
 
 pytestmark = pytest.mark.gpu
+GOLDEN_MEANS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "parity_means.npz")
 
 B = 32
 # thresholds.  Round 2 (all-bf16 encoder) measured max|dm| 2.4e-3 and 4.6 % of the indices off by one; the split-bf16
@@ -54,27 +60,34 @@ def _snr_db(a, ref):
 @pytest.fixture(scope="module")
 def c2(cuda):
     import bench
-    enc_prec, syn_prec = bench.PRECISIONS["bf16"]   # the bench's default mode is the one tested here
+    from conftest import golden_script
+    pm = golden_script("make_parity_means")
+    bench_input, fine_fc1 = pm.bench_input, pm.fine_fc1
+    enc_prec, syn_prec = bench.PRECISIONS[bench.DEFAULT_PRECISION]   # the bench's default mode is the one tested here
+    assert (enc_prec, syn_prec) == ("bf16x3", "f16")
     torch.manual_seed(0)
     enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
     torch.manual_seed(1)
     G = ic2.Generator(img_resolution=256).to(cuda).eval().requires_grad_(False)
-    x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+    x = bench_input(B, 256)
+    fx = np.load(GOLDEN_MEANS)
+    assert bytes(fx["c2_x_sha256"]) == hashlib.sha256(x.numpy().tobytes()).digest()
     with torch.no_grad():
         torch.manual_seed(5)  # the fine projector re-draws fc1 from the CPU RNG (ref :225-230)
         _, m16, _ = enc(x.to(cuda))
-        fc1 = (enc.fine_projector.fc1.weight.detach().cpu(), enc.fine_projector.fc1.bias.detach().cpu())
+        w1, b1 = fine_fc1()   # the draw the fixture's oracle means were computed with
+        assert torch.equal(enc.fine_projector.fc1.weight.detach().cpu(), w1)
+        assert torch.equal(enc.fine_projector.fc1.bias.detach().cpu(), b1)
         enc.set_precision("bf16")
         torch.manual_seed(5)
         _, m_allbf16, _ = enc(x.to(cuda))
         enc.set_precision(enc_prec)
-        sd = {k: v.detach().cpu() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
-        _, m_or, _ = oe.encoder_forward(sd, x, fine_fc1=fc1)
+        m_or = torch.from_numpy(fx["c2_means"])
         q16, i16 = ic2.quantize_uniform(m16, 8, return_indices=True)
         q_or = oe.quantize_uniform(m_or, 8)
         G.set_precision("fp32")
         ref = G.synthesis(q_or.to(cuda))
-        G.set_precision(syn_prec)
+        G.set_precision("bf16")
         img_e2e = G.synthesis(q16)
         img_syn = G.synthesis(q_or.to(cuda))
         G.set_precision("f16")
@@ -87,11 +100,11 @@ def c2(cuda):
 
 
 def test_c2_reference_reconstruction_is_the_oracle(c2):
-    """The fp32 reference reconstruction equals the CPU synthesis restatement (2 of the 32 images)."""
+    """The fp32 reference reconstruction equals the CPU synthesis restatement (1 of the 32 images)."""
     sd = {k: v.detach().float().cpu() for k, v in c2["G"].state_dict().items()}
-    r = sg3.synthesis_forward(sd, 256, c2["q_or"][:2], dtype=torch.float32)
-    err = (c2["ref"][:2].cpu() - r).abs().max().item()
-    print(f"[c2] fp32 path vs CPU oracle (2 images): max|err| = {err:.2e}")
+    r = sg3.synthesis_forward(sd, 256, c2["q_or"][:1], dtype=torch.float32)
+    err = (c2["ref"][:1].cpu() - r).abs().max().item()
+    print(f"[c2] fp32 path vs CPU oracle (1 image): max|err| = {err:.2e}")
     assert err < 1e-3
 
 

@@ -4,13 +4,18 @@ lrelu grids, the 81 / 51 / 32-channel tail), encoder split-bf16 'bf16x3' with th
 --precision bf16 / f16), at a batch the CPU oracle can afford.
 
 Reference path: stylegan3_hvae_full.py:295-329 (compress -> decompress), metric hvae_training.py:368-395.
-The oracle means come from oracle/encoder.py (pinned to the reference's encoder by tests/golden/encoder_full.npz);
+The oracle means of this input are the committed fixture tests/golden/parity_means.npz (made by
+tests/golden/make_parity_means.py from oracle/encoder.py, pinned to the reference's encoder by
+tests/golden/encoder_full.npz);
 the reference reconstruction is the fp32 path on the oracle's quantized latents, itself pinned to the CPU synthesis
 restatement at 1e-3 (test_gpu_path.py::test_synthesis_1024_fp32_within_1e3_of_oracle).
 Asserted as in test_gpu_c2_parity.py: index mismatches vs the oracle, synthesis-only and end-to-end SNR floors, the
 north-star PSNR delta at the README's 34 dB operating point, and a one-bf16-ulp-per-layer perturbation the floor
 catches.  Thresholds measured on MI355X are recorded in DESIGN.md (c).
 """
+import hashlib
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -40,18 +45,23 @@ def _snr_db(a, ref):
 @pytest.fixture(scope="module")
 def c4(cuda):
     import bench
-    enc_prec, syn_prec = bench.PRECISIONS["bf16"]
+    from conftest import golden_script
+    pm = golden_script("make_parity_means")
+    bench_input, fine_fc1 = pm.bench_input, pm.fine_fc1
+    enc_prec, syn_prec = bench.PRECISIONS[bench.DEFAULT_PRECISION]
     torch.manual_seed(0)
     enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(cuda).eval().requires_grad_(False)
     torch.manual_seed(1)
     G = ic2.Generator(img_resolution=1024).to(cuda).eval().requires_grad_(False)
-    x = torch.rand(B, 3, 1024, 1024, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+    x = bench_input(B, 1024)   # the first 2 images of bench.py's C4 batch
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "parity_means.npz"))
+    assert bytes(fx["c4_x_sha256"]) == hashlib.sha256(x.numpy().tobytes()).digest()
     with torch.no_grad():
         torch.manual_seed(5)  # the fine projector re-draws fc1 from the CPU RNG (ref :225-230)
         _, m_b, _ = enc(x.to(cuda))
-        fc1 = (enc.fine_projector.fc1.weight.detach().cpu(), enc.fine_projector.fc1.bias.detach().cpu())
-        sd = {k: v.detach().cpu() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
-        _, m_or, _ = oe.encoder_forward(sd, x, fine_fc1=fc1)
+        w1, b1 = fine_fc1()
+        assert torch.equal(enc.fine_projector.fc1.weight.detach().cpu(), w1)
+        m_or = torch.from_numpy(fx["c4_means"])
         q_b = ic2.quantize_uniform(m_b, 8)
         q_or = oe.quantize_uniform(m_or, 8)
         G.set_precision("fp32")

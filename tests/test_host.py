@@ -79,6 +79,23 @@ def test_round2_entry_points_validate_before_launch():
                     1e-5, f, 1 << 20, None, 0, -1, None) == 1
 
 
+def test_conv_gn_rejects_f16_operands():
+    """the fused conv + GroupNorm statistics path is bf16 halo-conv code.  f16 operands are
+    refused at the entry point (never reach the bf16 MFMA) and the fusion query never reports f16 as fusable."""
+    import ctypes
+    lib = nv.load()
+    f = ctypes.c_void_p(16)
+    for fuse in (-1, 0, 1):
+        # 64 -> 64 channels at 256^2: the halo conv's shape, fused on request in bf16
+        assert nv.query("ic2_conv3x3_gn_fuses", nv.F16, 8, 256, 256, 64, 64, 64, 3, 3, 1, 32, fuse) == 0
+        assert nv.query("ic2_conv3x3_gn_fwd", f, f, f, nv.F16, 8, 256, 256, 64, 64, 64, 3, 3, 1, f, 32, 1e-5, f,
+                        1 << 24, None, 0, fuse, None) == 1
+        assert b"dtype" in lib.ic2_last_error()
+        assert nv.query("ic2_conv3x3_gnin_gn_fwd", f, f, 0.2, f, f, nv.F16, 8, 256, 256, 64, 64, 64, 3, 3, 1, f, 32,
+                        1e-5, f, 1 << 24, None, 0, fuse, None) == 1
+    assert nv.query("ic2_conv3x3_gn_fuses", nv.BF16, 8, 256, 256, 64, 64, 64, 3, 3, 1, 32, 1) == 1
+
+
 def test_product_path_refuses_cpu_tensors():
     with pytest.raises(RuntimeError, match="ROCm"):
         ic2.quantize_uniform(torch.zeros(4, 16, 512))

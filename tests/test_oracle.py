@@ -195,3 +195,25 @@ def test_psnr_definition():
     ua, ub = om.to_uint8(a), om.to_uint8(b)
     mse = ((ua.astype(float) - ub.astype(float)) ** 2).mean()
     assert om.psnr(a, b) == pytest.approx(10 * math.log10(255 ** 2 / mse))
+
+
+def test_parity_means_fixture(golden_dir):
+    """tests/golden/parity_means.npz (the GPU parity tests' and bench.py's reference means) is what its generator
+    says: the inputs hash to the stored sha256, and the oracle re-derives the C2 means of the first 2 images."""
+    import hashlib
+    import image_compression_2_amd as ic2
+    from conftest import golden_script
+    pm = golden_script("make_parity_means")
+    fx = np.load(os.path.join(golden_dir, "parity_means.npz"))
+    for key, (n, res) in pm.INPUTS.items():
+        assert fx[f"{key}_means"].shape == (n, 16, 512)
+        x = pm.bench_input(n, res)
+        assert bytes(fx[f"{key}_x_sha256"]) == hashlib.sha256(x.numpy().tobytes()).digest(), key
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024)
+    sd = {k: v.detach() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
+    x = pm.bench_input(32, 256)[:2]
+    with torch.no_grad():
+        _, m, _ = oe.encoder_forward(sd, x, fine_fc1=pm.fine_fc1())
+    err = (m - torch.from_numpy(fx["c2_means"][:2])).abs().max().item()
+    assert err < 1e-5, err   # the same fp32 CPU computation (batch-size-dependent reduction order aside)
