@@ -37,6 +37,7 @@ _SIGS = {
     "ic2_code_record": [_P, _I, _I, _I, _P, _I64, _P, _P],
     "ic2_gumbel_softmax_quantize": [_P, _I64, _P, _I, _P, _F, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P,
                                     _P],
+    "ic2_gumbel_softmax_quantize_dseed": [_P, _I64, _P, _I, _P, _F, _I, _P, ctypes.c_uint64, _P, _P, _P, _P, _P],
     "ic2_bias_act": [_P, _P, _P, _I, _I64, _I64, _I64, _I, _F, _F, _F, _P],
     "ic2_upfirdn2d": [_P, _P, _I, _I64, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P],
     "ic2_filtered_lrelu": [_P, _P, _I, _I64, _I64, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _F,

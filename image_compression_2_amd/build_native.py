@@ -17,8 +17,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 INCLUDE = os.path.join(ROOT, "include")
-BUILD = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libic2ops.so")
+# diagnostic variants build elsewhere (IC2_BUILD_DIR / IC2_LIB_OUT, e.g. with IC2_EXTRA_CFLAGS=-D...) and are loaded
+# only under IC2_DEV=1 IC2_DEV_LIB=<path> (_native.py)
+BUILD = os.environ.get("IC2_BUILD_DIR", os.path.join(HERE, "_build"))
+LIB = os.environ.get("IC2_LIB_OUT", os.path.join(HERE, "libic2ops.so"))
 ARCH = os.environ.get("IC2_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wno-unused-result",

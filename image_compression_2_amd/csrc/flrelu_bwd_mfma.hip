@@ -90,13 +90,21 @@ __device__ __forceinline__ float fb_dact(float u, float ga, float slope, float g
   return l < lim ? ga * gs : 0.f;
 }
 
+// diagnostic build switch: 1 = the item's oscale row DMA'd into a 64-B LDS slot by four lanes of the
+// last wave with the ring groups, exactly as the forward strip kernel DMAs its post-scale row (flrelu_mfma.hip
+// flrelu_mfma3_kernel ps_lds), retired by the item-top vmcnt + barrier; 0 (default) = a plain global load per lane
+#ifndef FBM_OS_DMA
+#define FBM_OS_DMA 0
+#endif
+
 template <int U, int TJX>
 __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, int nitems, int nseg, int seg_len) {
   using G = FbmGeom<U, TJX>;
   constexpr int NW = G::NW, NT = 64 * NW, NBT = G::NBT, NBX = G::NBX, NINX = G::NINX, NOX = G::NOX, S = G::S;
   constexpr int OCW = G::OCW, NGX = G::NGX;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW + (FBM_OS_DMA ? 16 : 0)];
   uint32_t* const xring = lds;
+  uint32_t* const os_lds = lds + G::LDS_DW;  // FBM_OS_DMA: the item's oscale row (its own slot)
   uint32_t* const gring = lds + G::XR_DW;
   uint32_t* const v_img = gring + G::GR_DW;  // V (f16), then P (bf16) row by row
   uint32_t* const a_img = v_img + G::V_DW;   // GAv (bf16)
@@ -196,6 +204,11 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
     for (int q = 0; q < NGX; ++q) load_xgroup(n, o.iy0, o.ix0, c0, q);
 #pragma unroll
     for (int q = 0; q < 3; ++q) load_ggroup(n, o.oy0, o.ox0, c0, q);
+    if (FBM_OS_DMA && a.oscale != nullptr && wave == NW - 1 && lane < 4) {  // 64 B: oscale[n][c0 .. c0 + 16)
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.oscale + (int64_t)n * a.c_p + c0), 0, 64, 0x00020000);
+      fm_dma16(prs, lane * 16, os_lds);
+    }
   };
   if (slot < nitems) load_item(slot);
   __syncthreads();  // taps
@@ -249,8 +262,12 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
     // land at the first tile's epilogue, behind the ring DMAs issued by then)
     float4 osv = make_float4(1.f, 1.f, 1.f, 1.f);
     if (a.oscale) {
-      osv = *reinterpret_cast<const float4*>(a.oscale + (int64_t)n * a.c_p + c0 + 4 * g);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (FBM_OS_DMA) {
+        osv = *reinterpret_cast<const float4*>(os_lds + 4 * g);  // landed: the wait + barrier above
+      } else {
+        osv = *reinterpret_cast<const float4*>(a.oscale + (int64_t)n * a.c_p + c0 + 4 * g);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      }
     }
     const float osc[4] = {osv.x, osv.y, osv.z, osv.w};
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(

@@ -182,7 +182,8 @@ template <int KPL>
 __global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float* __restrict__ z, int64_t n,
                                                              const float* __restrict__ cb, int k,
                                                              const float* __restrict__ log_tau, float tau_const,
-                                                             int hard, uint64_t seed, uint64_t offset,
+                                                             int hard, uint64_t seed,
+                                                             const uint64_t* __restrict__ seed_dev, uint64_t offset,
                                                              const float* __restrict__ noise,
                                                              float* __restrict__ disc, int64_t* __restrict__ idx,
                                                              float* __restrict__ prob_sum) {
@@ -200,7 +201,10 @@ __global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float* __rest
   float psum[KPL];
 #pragma unroll
   for (int j = 0; j < KPL; ++j) psum[j] = 0.f;
-  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  // seed_dev: the seed drawn on the device generator by the caller (no host sync, and torch's CPU stream -- which the
+  // reference's fine projector re-creates fc1 from -- is not consumed)
+  const uint64_t sd = seed_dev ? seed_dev[0] : seed;
+  const uint2 key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
   for (int64_t i = (int64_t)blockIdx.x * 4 + wv; i < n; i += nwaves) {
     const float v = z[i];
     float y[KPL];
@@ -293,10 +297,10 @@ __global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float* __rest
 
 }  // namespace ic2
 
-extern "C" int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k,
-                                           const float* log_tau, float tau, int hard, uint64_t seed,
-                                           uint64_t offset, const float* gumbel_noise, float* disc_out,
-                                           int64_t* idx_out, float* prob_sum_out, void* stream) {
+static int gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k, const float* log_tau,
+                                   float tau, int hard, uint64_t seed, const uint64_t* seed_dev, uint64_t offset,
+                                   const float* gumbel_noise, float* disc_out, int64_t* idx_out, float* prob_sum_out,
+                                   void* stream) {
   IC2_CHECK_ARG(n >= 0 && k >= 1 && k <= 1024, "gumbel_softmax_quantize: need 1 <= k <= 1024 (k=%d)", k);
   IC2_CHECK_ARG(n == 0 || (z && codebook && disc_out), "gumbel_softmax_quantize: null pointer");
   IC2_CHECK_ARG(log_tau || tau > 0.f, "gumbel_softmax_quantize: temperature must be positive");
@@ -306,7 +310,7 @@ extern "C" int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const floa
   hipStream_t s = ic2::as_stream(stream);
 #define IC2_GS(KPL)                                                                                                   \
   hipLaunchKernelGGL(ic2::gumbel_softmax_kernel<KPL>, dim3((unsigned)g), dim3(256), 0, s, z, n, codebook, k, log_tau, \
-                     tau, hard, seed, offset, gumbel_noise, disc_out, idx_out, prob_sum_out)
+                     tau, hard, seed, seed_dev, offset, gumbel_noise, disc_out, idx_out, prob_sum_out)
   if (k <= 64) IC2_GS(1);
   else if (k <= 128) IC2_GS(2);
   else if (k <= 256) IC2_GS(4);
@@ -315,6 +319,24 @@ extern "C" int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const floa
 #undef IC2_GS
   IC2_CHECK_LAUNCH("gumbel_softmax_quantize");
   return IC2_OK;
+}
+
+extern "C" int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k,
+                                           const float* log_tau, float tau, int hard, uint64_t seed,
+                                           uint64_t offset, const float* gumbel_noise, float* disc_out,
+                                           int64_t* idx_out, float* prob_sum_out, void* stream) {
+  return gumbel_softmax_quantize(z, n, codebook, k, log_tau, tau, hard, seed, nullptr, offset, gumbel_noise, disc_out,
+                                 idx_out, prob_sum_out, stream);
+}
+
+extern "C" int ic2_gumbel_softmax_quantize_dseed(const float* z, int64_t n, const float* codebook, int k,
+                                                 const float* log_tau, float tau, int hard, const int64_t* seed_dev,
+                                                 uint64_t offset, const float* gumbel_noise, float* disc_out,
+                                                 int64_t* idx_out, float* prob_sum_out, void* stream) {
+  IC2_CHECK_ARG(seed_dev != nullptr || gumbel_noise != nullptr || n == 0,
+                "gumbel_softmax_quantize_dseed: seed_dev is null");
+  return gumbel_softmax_quantize(z, n, codebook, k, log_tau, tau, hard, 0, reinterpret_cast<const uint64_t*>(seed_dev),
+                                 offset, gumbel_noise, disc_out, idx_out, prob_sum_out, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

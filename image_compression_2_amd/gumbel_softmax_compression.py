@@ -4,9 +4,13 @@ GumbelSoftmaxDiscretization keeps the reference's buffers/parameters (``codebook
 ``log_temperature``, ``usage``) and signatures; its forward is ONE fused HIP kernel
 (``ic2_gumbel_softmax_quantize``) instead of the reference's chain of [N*8192, K] fp32 tensors.
 Indices are bit-exact (fp32 |z - c| argmin, first index on ties, ref :97, :118).  The Gumbel noise
-comes from an in-kernel Philox stream seeded from torch's CPU generator: the same distribution as
-``F.gumbel_softmax``, not the same stream (the reference's noisy outputs are RNG-dependent anyway,
-SURVEY.md 0 quirk 3); compress()/decompress() are deterministic and bit-exact.
+comes from an in-kernel Philox stream whose seed is drawn on the device generator (as ``F.gumbel_softmax`` draws on
+z's device): the same distribution as the reference's noise, not the same stream (the reference's noisy outputs are
+RNG-dependent anyway), and torch's CPU stream -- which the encoder's fine projector re-creates
+fc1 from -- advances exactly as the reference's.  The device generator's offset advances by a different amount than
+the reference's [N*8192, K] exponential_ draw (only later device draws, e.g. the reparameterisation noise of w_plus,
+see that); compress()/decompress() are deterministic and bit-exact, and compress() skips the noise entirely (its
+indices are the exact argmin) while still counting `usage` in training mode as the reference's does.
 Forward is inference-only: it runs in grad mode, but a backward through the kernel raises (training is out of
 scope).
 """
@@ -91,9 +95,13 @@ class GumbelSoftmaxDiscretization(nn.Module):
         if gumbel_noise is not None:
             gumbel_noise = gumbel_noise.to(torch.float32).contiguous()
             assert gumbel_noise.shape == (m, k)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # CPU generator: no device sync
-        nv.call("ic2_gumbel_softmax_quantize", nv.ptr(z), m, nv.ptr(self.codebook), k,
-                nv.ptr(self.log_temperature.detach()), 1.0, int(bool(hard)), seed, 0, nv.ptr(gumbel_noise),
+        # the Philox seed is drawn on the DEVICE generator (F.gumbel_softmax draws its noise on z's device, ref
+        # :103-108) and read by the kernel from device memory: no host sync, and torch's CPU stream -- from which the
+        # fine projector re-creates fc1 on every encoder call (stylegan3_hvae_full.py:225-230) -- advances exactly as
+        # the reference's does
+        seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=z.device)
+        nv.call("ic2_gumbel_softmax_quantize_dseed", nv.ptr(z), m, nv.ptr(self.codebook), k,
+                nv.ptr(self.log_temperature.detach()), 1.0, int(bool(hard)), nv.ptr(seed), 0, nv.ptr(gumbel_noise),
                 nv.ptr(disc), nv.ptr(idx), nv.ptr(psum), nv.stream_of(z))
         if self.training:
             hist = torch.zeros(k, dtype=torch.int32, device=z.device)
@@ -152,7 +160,14 @@ class GumbelSoftmaxCompressor(nn.Module):
         first index on ties, gumbel_softmax_compression.py:229) without its device -> host copy (:235)."""
         with torch.no_grad():
             w_plus, means, _ = self.encoder(x)
-            indices = codebook_argmin(means, self.discretization.codebook)
+            disc = self.discretization
+            if disc.training:
+                # the reference's compress runs discretization(means, hard=True), which in training mode adds the
+                # batch's argmin indices to `usage` (:121-123); the indices are the same exact argmin
+                indices, hist = codebook_argmin(means, disc.codebook, hist=True)
+                disc.usage += hist.to(disc.usage.dtype)
+            else:
+                indices = codebook_argmin(means, disc.codebook)
             batch_size, num_ws, w_dim = w_plus.shape
             return indices.reshape(batch_size, num_ws, w_dim)
 

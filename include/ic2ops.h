@@ -66,6 +66,14 @@ int ic2_codebook_lookup(const int64_t* codes, int64_t n, const float* codebook, 
 int ic2_gumbel_softmax_quantize(const float* z, int64_t n, const float* codebook, int k, const float* log_tau,
                                 float tau, int hard, uint64_t seed, uint64_t offset, const float* gumbel_noise,
                                 float* disc_out, int64_t* idx_out, float* prob_sum_out, void* stream);
+/* The same with the Philox seed read from device memory (*seed_dev, e.g. a torch.randint drawn on the device
+ * generator as F.gumbel_softmax draws its noise on the tensor's device, gumbel_softmax_compression.py:103-108): no
+ * host sync, and the CPU generator -- which the reference's fine projector re-creates fc1 from on every call,
+ * stylegan3_hvae_full.py:225-230 -- is left untouched. */
+int ic2_gumbel_softmax_quantize_dseed(const float* z, int64_t n, const float* codebook, int k, const float* log_tau,
+                                      float tau, int hard, const int64_t* seed_dev, uint64_t offset,
+                                      const float* gumbel_noise, float* disc_out, int64_t* idx_out,
+                                      float* prob_sum_out, void* stream);
 
 /* Per-batch code record (SURVEY.md 8e metric record; usage / perplexity over the batch,
  * gumbel_softmax_compression.py:121-127): kind 0 = f32 latents from ic2_quantize_uniform at `bits` (code =

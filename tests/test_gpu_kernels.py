@@ -641,3 +641,43 @@ def test_flrelu_strip_segmentation_invariant(cuda, gen256_bf16_layers, layer):
     torch.cuda.synchronize()
     assert torch.isfinite(full.float()).all()
     assert torch.equal(full, parts)
+
+
+@pytest.mark.parametrize("layer", [10, 13])
+def test_flrelu_strip_post_scale_rows_across_items(cuda, gen256_bf16_layers, layer):
+    """the strip kernel DMAs each item's post-scale row (16 floats) into a 64-B LDS slot by four
+    lanes of its last wave, together with the item's first input rows, while the previous item is still being
+    computed.  Here every workgroup runs at least two items (n 4, 32 channels: more strips x segments than resident
+    workgroups), up 4 (L10) and up 2 (L13), and the post-scale rows are distinct per sample and per channel, so a
+    row that landed late, early or in the wrong slot shows up against the fp64 composition."""
+    import ctypes
+    L = gen256_bf16_layers[layer]
+    n, c_p = 4, 32
+    conv = int(L.in_size[0]) + 2
+    s_out = int(L.out_size[0])
+    tiles_x, tiles_y = -(-s_out // 32), -(-s_out // 16)
+    strips = n * tiles_x * (c_p // 16)
+    nseg = min(tiles_y, max(1, -(-2 * 512 // strips)))
+    seg_len = -(-tiles_y // nseg)
+    items = strips * -(-tiles_y // seg_len)
+    assert items > 512, items   # > one item per resident workgroup (256 CUs x 2)
+    g = torch.Generator().manual_seed(110 + layer)
+    x = (torch.randn(n, c_p, conv, conv, generator=g) * 2).to(torch.float16).float()
+    x[:, :, :3, :5] = 300.0
+    ps = 0.5 + torch.arange(c_p, dtype=torch.float32)[None, :] / 16 + 0.37 * torch.arange(n, dtype=torch.float32)[:, None]
+    xb = x.to(torch.float16).reshape(n, c_p // 16, 16, conv, conv).permute(0, 1, 3, 4, 2).contiguous().to(cuda)
+    out = torch.full((n, s_out, s_out, c_p), float("nan"), device=cuda, dtype=torch.bfloat16)
+    psd = ps.to(cuda)
+    nv.call("ic2_flrelu_nhwc16", nv.ptr(xb), nv.ptr(out), nv.F16, nv.BF16, n, c_p, conv, conv, s_out, s_out,
+            L._fu.ctypes.data_as(ctypes.c_void_p), L._fu.shape[0], L._fd.ctypes.data_as(ctypes.c_void_p),
+            L._fd.shape[0], None, L.up_factor, L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0,
+            nv.ptr(psd), nv.stream_of(xb))
+    torch.cuda.synchronize()
+    r = sg3.filtered_lrelu(x.double(), torch.from_numpy(L._fu).double(), torch.from_numpy(L._fd).double(), None,
+                           up=L.up_factor, down=L.down_factor, padding=L.padding, gain=np.sqrt(2), slope=0.2,
+                           clamp=256.0) * ps.double()[:, :, None, None]
+    y = out.float().cpu().permute(0, 3, 1, 2).double()
+    # per (sample, channel): the ratio of the output to the unscaled reference must be that row's scale
+    err = ((y - r).abs().amax(dim=(2, 3)) / (1 + r.abs().amax(dim=(2, 3))))
+    print(f"[flrelu post-scale rows L{layer}] items {items}, worst per-(n, c) relative error {err.max().item():.2e}")
+    assert err.max().item() < 2e-2

@@ -329,6 +329,46 @@ def test_gumbel_compressor_round_trip(cuda, gen256):
     assert _maxdiff(img, ref) < 1e-3
 
 
+def test_gumbel_encode_leaves_the_cpu_stream_to_the_fine_projector(cuda, gen256):
+    """The discretization draws its noise seed on the device (as F.gumbel_softmax draws on z's device,
+    gumbel_softmax_compression.py:103-108), so torch's CPU stream advances only through the fine projector's fc1
+    re-creation (stylegan3_hvae_full.py:225-230), exactly as the reference's: under one seed, the fc1 of a first and
+    a second encode() are the reference's 1st and 2nd nn.Linear(128, 256) draws, and the second call's slots 12-15
+    are the oracle's with that fc1.  compress() in training mode counts usage as the reference's
+    forward(hard=True) does (:121-123); in eval mode it does not."""
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024).to(cuda).eval()
+    comp = ic2.GumbelSoftmaxCompressor(enc, gen256).to(cuda).eval()
+    x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(12)) * 2 - 1)
+    torch.manual_seed(11)
+    lin1, lin2 = torch.nn.Linear(128, 256), torch.nn.Linear(128, 256)   # the reference's two draws
+    torch.manual_seed(11)
+    comp.encode(x.to(cuda))
+    assert torch.equal(enc.fine_projector.fc1.weight.detach().cpu(), lin1.weight.detach())
+    comp.encode(x.to(cuda))
+    assert torch.equal(enc.fine_projector.fc1.weight.detach().cpu(), lin2.weight.detach())
+    assert torch.equal(enc.fine_projector.fc1.bias.detach().cpu(), lin2.bias.detach())
+    # the second call's continuous slots 12-15 (replayed: seed, one encode(), then the encoder alone)
+    torch.manual_seed(11)
+    comp.encode(x.to(cuda))
+    _, m2, _ = enc(x.to(cuda))
+    sd = {k: v.detach().cpu() for k, v in enc.state_dict().items() if not k.startswith("fine_projector.fc1")}
+    _, m_or, _ = oe.encoder_forward(sd, x, fine_fc1=(lin2.weight.detach(), lin2.bias.detach()))
+    err = _maxdiff(m2[:, 12:], m_or[:, 12:])
+    print(f"[gumbel] second encode(): slots 12-15 vs the oracle with the reference's 2nd fc1 draw: {err:.2e}")
+    assert err < 1e-4
+    # usage: counted by compress() in training mode only
+    disc = comp.discretization
+    disc.usage.zero_()
+    comp.compress(x.to(cuda))
+    assert float(disc.usage.sum()) == 0.0
+    disc.train()
+    codes = comp.compress(x.to(cuda))
+    hist = torch.bincount(codes.reshape(-1), minlength=disc.n_embeddings).float()
+    assert torch.equal(disc.usage.cpu(), hist)
+    disc.eval()
+
+
 def test_codebook_container_round_trip(cuda, gen256, tmp_path, golden_dir):
     """GumbelSoftmaxCompressor.save_compressed / load_compressed (ref gumbel_softmax_compression.py:266-319):
     same keys and stats as the reference's container, codes that decode to the same image as decompress(),
