@@ -490,9 +490,13 @@ def run(args):
             from image_compression_2_amd import training as ict
             opt = ict.make_optimizer(enc, lr=1e-4)
             w_avg = G.mapping.w_avg.view(1, 1, -1)
+            # BASELINE config 5 is fp16: the reference's autocast + GradScaler (stylegan3_hvae_full.py:487,669,693-696)
+            # as f16 encoder / synthesis with a dynamic loss scaler
+            scaler = ict.make_f16(comp) if syn_prec == "f16" else None
 
             def train_step():
-                losses = ict.train_step(comp, x, opt, w_avg, rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01)
+                losses = ict.train_step(comp, x, opt, w_avg, rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01,
+                                        scaler=scaler)
                 vec = torch.cat([(losses["rec_loss"].double() * batch).view(1),
                                  (losses["kl_loss"].double() * batch).view(1), counts[1:]])
                 return icd.allreduce_sum(vec, device=dev)
@@ -580,6 +584,9 @@ def run(args):
                              parallelism=f"dp{world} (batch-sharded, RCCL gradient all_reduce)")
         out["last_step_losses"] = {"rec_loss": round(vec[0].item() / vec[2].item(), 6),
                                    "kl_loss": round(vec[1].item() / vec[2].item(), 4)}
+        if syn_prec == "f16":
+            out["config"]["loss_scaler"] = "torch.amp.GradScaler (dynamic, init 2^16; the reference's fp16 branch)"
+            out["dtype"] = "f16 (encoder + synthesis, f32 accumulate and master weights)"
     else:
         from image_compression_2_amd import metrics as icm
         out["psnr_db_vs_input"] = round(icm.psnr_from_sums(vec[0].item(), vec[1].item()), 4)

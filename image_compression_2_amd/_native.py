@@ -270,15 +270,16 @@ def torch_dtype(precision):
     raise ValueError(f"precision must be 'fp32', 'bf16' or 'f16', got {precision!r}")
 
 
-ENCODER_PRECISIONS = ("fp32", "bf16", "bf16x3")
+ENCODER_PRECISIONS = ("fp32", "bf16", "bf16x3", "f16")
 
 
 def encoder_dtype(precision):
     """HVAE_VGG_Encoder precision -> (activation storage dtype, split).  'bf16x3' = split bf16 (ic2ops.h
-    IC2_BF16X3): bf16 MFMA operands [hi | hi | lo] x [hi | lo | hi], f32 conv outputs, GroupNorm in f32."""
+    IC2_BF16X3): bf16 MFMA operands [hi | hi | lo] x [hi | lo | hi], f32 conv outputs, GroupNorm in f32.  'f16': f16
+    activations and MFMA operands (the f16 training precision, BASELINE config 5's fp16; loss-scaled)."""
     if precision == "bf16x3":
         return torch.bfloat16, True
-    if precision in ("fp32", "bf16"):
+    if precision in ("fp32", "bf16", "f16"):
         return torch_dtype(precision), False
     raise ValueError(f"encoder precision must be one of {ENCODER_PRECISIONS}, got {precision!r}")
 

@@ -9,9 +9,13 @@
 //   ic2_gap_bwd : d(mean over H x W) / dx  (the HierarchyProjector's AdaptiveAvgPool2d(1))
 #include "common.h"
 
+#include <type_traits>
+
 namespace ic2 {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 wg_bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 wg_f16x8;
+typedef _Float16 bw_h2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((ext_vector_type(4))) float wg_f32x4;
 typedef short wg_s4 __attribute__((ext_vector_type(4)));
 
@@ -122,7 +126,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (std::is_same<T, _Float16>::value)   // the f16 training path: f16 operands, same fragments
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(wg_f16x8, af[i]),
+                                                               __builtin_bit_cast(wg_f16x8, bfr[j]), acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
     } else {
       // f32: 16x16x4 MFMA, lane (g, li) holds A[m = li][k = g] / B[k = g][n = li] per 4-pixel step (exact fp32)
       const float* fdy = reinterpret_cast<const float*>(sdy);
@@ -208,6 +218,16 @@ __device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) {
     v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
   }
 }
+__device__ __forceinline__ void ld8(const _Float16* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bw_h2 h = __builtin_bit_cast(bw_h2, w[k]);
+    v[2 * k] = (float)h.x;
+    v[2 * k + 1] = (float)h.y;
+  }
+}
 __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -216,6 +236,13 @@ __device__ __forceinline__ void st8(bf16_t* p, const float (&v)[8]) {
   uint32_t w[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+// f16 (the f16 training path): IEEE conversion, so a loss-scaled gradient that overflows reaches the scaler as inf
+__device__ __forceinline__ void st8(_Float16* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = __builtin_bit_cast(uint32_t, bw_h2{(_Float16)v[2 * k], (_Float16)v[2 * k + 1]});
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 // dL/da of output pixel p (channels cc0 .. cc0 + 7): dout, or a quarter of the pooled gradient (0 on a floor-dropped
@@ -410,7 +437,9 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const float* __restrict__ 
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int cc = (int)(e % c_p);
     const int nn = (int)(e / ((int64_t)hw * c_p));
-    st(dx + e, cc < c ? dp[(int64_t)nn * c + cc] * inv : 0.f);
+    const float v = cc < c ? dp[(int64_t)nn * c + cc] * inv : 0.f;
+    if constexpr (std::is_same<TO, _Float16>::value) dx[e] = (_Float16)v;   // IEEE (the scaler sees an overflow)
+    else st(dx + e, v);
   }
 }
 
@@ -439,6 +468,13 @@ template <typename T> __device__ __forceinline__ void sb_st2(T* p, float2 v);
 template <> __device__ __forceinline__ void sb_st2<float>(float* p, float2 v) { *reinterpret_cast<float2*>(p) = v; }
 template <> __device__ __forceinline__ void sb_st2<bf16_t>(bf16_t* p, float2 v) {
   *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+}
+template <> __device__ __forceinline__ float2 sb_ld2<_Float16>(const _Float16* p) {
+  const bw_h2 h = *reinterpret_cast<const bw_h2*>(p);
+  return make_float2((float)h.x, (float)h.y);
+}
+template <> __device__ __forceinline__ void sb_st2<_Float16>(_Float16* p, float2 v) {
+  *reinterpret_cast<bw_h2*>(p) = bw_h2{(_Float16)v.x, (_Float16)v.y};
 }
 
 template <typename T>
@@ -522,6 +558,9 @@ extern "C" int ic2_scale_nhwc(const void* x, const float* xscale, void* a, int d
     hipLaunchKernelGGL(scale_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, xscale, (float*)a, hw, c_p);
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(scale_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, xscale, (bf16_t*)a, hw, c_p);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(scale_fwd_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, xscale, (_Float16*)a, hw,
+                       c_p);
   else
     IC2_CHECK_ARG(false, "scale_nhwc: bad dtype %d", dtype);
   IC2_CHECK_LAUNCH("scale_nhwc");
@@ -544,6 +583,9 @@ extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xs
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(scale_bwd_kernel<bf16_t>, dim3(n * nchunks), dim3(256), lds, s, (const bf16_t*)da,
                        (const bf16_t*)x, xscale, (bf16_t*)dx, part, hw, c_p, nchunks, chunk_pix);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(scale_bwd_kernel<_Float16>, dim3(n * nchunks), dim3(256), lds, s, (const _Float16*)da,
+                       (const _Float16*)x, xscale, (_Float16*)dx, part, hw, c_p, nchunks, chunk_pix);
   else
     IC2_CHECK_ARG(false, "scale_bwd_nhwc: bad dtype %d", dtype);
   IC2_CHECK_LAUNCH("scale_bwd_nhwc");
@@ -565,7 +607,7 @@ extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int 
 extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
                               int cout_p, int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream) {
   IC2_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null pointer");
-  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16, "conv_wgrad: bad dtype %d", dtype);
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16, "conv_wgrad: bad dtype %d", dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
                 "conv_wgrad: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
   IC2_CHECK_ARG(n > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0, "conv_wgrad: bad geometry");
@@ -586,6 +628,7 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)(ceil_div(cout_p, WG_BO) * a.j_tiles), (unsigned)splits);
   if (dtype == IC2_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else if (dtype == IC2_F16) hipLaunchKernelGGL(wgrad_kernel<_Float16>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, s, workspace, dw, total, splits);
   IC2_CHECK_LAUNCH("conv_wgrad");
@@ -608,9 +651,11 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
   IC2_CHECK_ARG(!pool || (h >= 2 && w >= 2), "gn_lrelu_pool_bwd: pooling needs H, W >= 2");
   IC2_CHECK_ARG(c_p % 8 == 0 && n <= 65535, "gn_lrelu_pool_bwd: c_p must be a multiple of 8 (n <= 65535)");
   IC2_CHECK_ARG(ws_floats >= ic2_gn_lrelu_pool_bwd_floats(n, h, w, c_p, groups), "gn_lrelu_pool_bwd: workspace too small");
-  IC2_CHECK_ARG((dtype_y == IC2_F32 || dtype_y == IC2_BF16) && (dtype_dout == IC2_F32 || dtype_dout == IC2_BF16) &&
-                    (dtype_dy == IC2_F32 || dtype_dy == IC2_BF16),
-                "gn_lrelu_pool_bwd: bad dtypes");
+  const bool f16 = dtype_y == IC2_F16 || dtype_dout == IC2_F16 || dtype_dy == IC2_F16;
+  IC2_CHECK_ARG(f16 ? (dtype_y == IC2_F16 && dtype_dout == IC2_F16 && dtype_dy == IC2_F16)
+                    : ((dtype_y == IC2_F32 || dtype_y == IC2_BF16) && (dtype_dout == IC2_F32 || dtype_dout == IC2_BF16) &&
+                       (dtype_dy == IC2_F32 || dtype_dy == IC2_BF16)),
+                "gn_lrelu_pool_bwd: bad dtypes (f16 only as f16 y, dout and dy)");
   const int nchunks = (int)ceil_div((int64_t)h * w, GNB_CHUNK);
   float* part = workspace;
   double* ab = reinterpret_cast<double*>(workspace + (((int64_t)n * c_p * nchunks * 2 + 1) / 2) * 2);
@@ -621,7 +666,8 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
   const int ps4 = 256 / (c_p / 8 < 256 ? c_p / 8 : 256);
   const int64_t pblocks = ceil_div(ceil_div((int64_t)h * w, ps4), 4);
   const dim3 apply_grid((unsigned)(pblocks < 1 ? 1 : (pblocks > 65535 ? 65535 : pblocks)), (unsigned)n);
-#define IC2_GNB(TY, TD)                                                                                          \
+#define IC2_GNB(TY, TD) IC2_GNB_O(TY, TD, bf16_t)
+#define IC2_GNB_O(TY, TD, TOB)                                                                                   \
   do {                                                                                                           \
     hipLaunchKernelGGL((gnb_partial_kernel<TY, TD>), dim3((unsigned)(n * nchunks)), dim3(256), 0, s, (const TY*)y, \
                        (const TD*)dout, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool, nchunks, part);   \
@@ -635,15 +681,17 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
                          (const TD*)dout, (float*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,    \
                          s12);                                                                                   \
     else                                                                                                         \
-      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, bf16_t>), apply_grid, dim3(256), 0, s, (const TY*)y,            \
-                         (const TD*)dout, (bf16_t*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,   \
+      hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, TOB>), apply_grid, dim3(256), 0, s, (const TY*)y,               \
+                         (const TD*)dout, (TOB*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,      \
                          s12);                                                                                   \
   } while (0)
-  if (dtype_y == IC2_F32 && dtype_dout == IC2_F32) IC2_GNB(float, float);
+  if (f16) IC2_GNB_O(_Float16, _Float16, _Float16);
+  else if (dtype_y == IC2_F32 && dtype_dout == IC2_F32) IC2_GNB(float, float);
   else if (dtype_y == IC2_F32) IC2_GNB(float, bf16_t);
   else if (dtype_dout == IC2_F32) IC2_GNB(bf16_t, float);
   else IC2_GNB(bf16_t, bf16_t);
 #undef IC2_GNB
+#undef IC2_GNB_O
   IC2_CHECK_LAUNCH("gn_lrelu_pool_bwd");
   return IC2_OK;
 }
@@ -656,6 +704,8 @@ extern "C" int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int
                                            (float*)dx, n, hw, c_p, c);
   else if (dtype == IC2_BF16) hipLaunchKernelGGL(gap_bwd_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, s,
                                                  dpooled, (bf16_t*)dx, n, hw, c_p, c);
+  else if (dtype == IC2_F16) hipLaunchKernelGGL(gap_bwd_kernel<_Float16>, dim3(grid_for(total)), dim3(256), 0, s,
+                                                dpooled, (_Float16*)dx, n, hw, c_p, c);
   else IC2_CHECK_ARG(false, "gap_bwd: bad dtype");
   IC2_CHECK_LAUNCH("gap_bwd");
   return IC2_OK;

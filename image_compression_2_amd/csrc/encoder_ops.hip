@@ -89,6 +89,12 @@ template <> __device__ __forceinline__ float2 ld2<bf16_t>(const bf16_t* p) {
   const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
   return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
 }
+// f16 activations: the encoder's f16 training precision (the reference's fp16 autocast, BASELINE config 5)
+typedef _Float16 ic2_h2 __attribute__((ext_vector_type(2)));
+template <> __device__ __forceinline__ float2 ld2<_Float16>(const _Float16* p) {
+  const ic2_h2 v = *reinterpret_cast<const ic2_h2*>(p);
+  return make_float2((float)v.x, (float)v.y);
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ y, int hw, int c_p, int c, int groups,
@@ -193,6 +199,16 @@ template <> __device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float (
     v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
   }
 }
+template <> __device__ __forceinline__ void ld8<_Float16>(const _Float16* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const ic2_h2 h = __builtin_bit_cast(ic2_h2, w[k]);
+    v[2 * k] = (float)h.x;
+    v[2 * k + 1] = (float)h.y;
+  }
+}
 template <typename T> __device__ __forceinline__ void st8(T* p, const float (&v)[8]);
 template <> __device__ __forceinline__ void st8<float>(float* p, const float (&v)[8]) {
   reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -205,6 +221,14 @@ template <> __device__ __forceinline__ void st8<bf16_t>(bf16_t* p, const float (
   u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
   u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
   *reinterpret_cast<uint4*>(p) = u;
+}
+template <> __device__ __forceinline__ void st8<_Float16>(_Float16* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)  // activations saturate at the f16 range (Elem<_Float16>, the synthesis's f16 mode)
+    w[k] = __builtin_bit_cast(uint32_t, ic2_h2{(_Float16)__builtin_amdgcn_fmed3f(v[2 * k], -65504.f, 65504.f),
+                                               (_Float16)__builtin_amdgcn_fmed3f(v[2 * k + 1], -65504.f, 65504.f)});
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // eight consecutive channels ch0 .. ch0+7 of pixel `pix` (tensor-global pixel index) with logical stride c_p
@@ -719,6 +743,9 @@ extern "C" int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int
   else if (dtype == IC2_BF16)
     hipLaunchKernelGGL(gn_partial_kernel<bf16_t>, dim3(n * nchunks), dim3(256), lds, s, (const bf16_t*)y, hw, c_p, c,
                        groups, nchunks, chunk_pix, part);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(gn_partial_kernel<_Float16>, dim3(n * nchunks), dim3(256), lds, s, (const _Float16*)y, hw, c_p,
+                       c, groups, nchunks, chunk_pix, part);
   else
     IC2_CHECK_ARG(false, "group_norm_stats: bad dtype");
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups,
@@ -859,6 +886,7 @@ extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dty
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_F32) IC2_GN_LAUNCH(bf16_t, float);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(float, bf16_t);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16X3) IC2_GN_LAUNCH(float, bf16x3_t);
+  else if (dtype_in == IC2_F16 && dtype_out == IC2_F16) IC2_GN_LAUNCH(_Float16, _Float16);
   else IC2_CHECK_ARG(false, "gn_lrelu_pool: bad dtypes");
 #undef IC2_GN_LAUNCH
   IC2_CHECK_LAUNCH("gn_lrelu_pool");
@@ -881,6 +909,8 @@ extern "C" int ic2_global_avg_pool(const void* x, int dtype, int n, int hw, int 
     hipLaunchKernelGGL(gap_partial_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, hw, c_p, nchunks, part);
   else if (dtype == IC2_BF16X3)
     hipLaunchKernelGGL(gap_partial_kernel<bf16x3_t>, grid, dim3(256), 0, s, (const bf16x3_t*)x, hw, c_p, nchunks, part);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(gap_partial_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, hw, c_p, nchunks, part);
   else
     IC2_CHECK_ARG(false, "global_avg_pool: bad dtype");
   hipLaunchKernelGGL(gap_finalize_kernel, dim3((unsigned)ceil_div(c, 16), (unsigned)n), dim3(256), 0, s, part, n, c_p,

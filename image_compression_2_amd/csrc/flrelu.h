@@ -23,7 +23,15 @@ struct FlrArgs {
   float gdg[12];     // down taps * gain (horizontal pass, right after the activation)
   float gu[24];  // flipped (unless flip_filter) and scaled by `up` (sqrt of the up^2 gain per pass)
   float gd[12];  // flipped (unless flip_filter)
+  // MFMA clamp-split kernels (finite lim): the horizontal passes' taps with the clamp scaling folded in on the host
+  // before the joint f16 rounding (f16_round_taps), so each polyphase group keeps its DC gain
+  float guh[24];  // gu / lim
+  float gdgl[12];  // gdg * lim
 };
+
+// taps -> f16-representable values, rounded jointly per group t mod stride_groups (minimal group sum error):
+// the MFMA kernels' f16 FIR taps (flrelu.hip; shared with the MFMA backward, flrelu_bwd.hip)
+void f16_round_taps(const float* exact, float* out, int n, int stride_groups);
 
 // NHWC or channel-blocked NHWC16 (strides in a), f16 (in_f16) or bf16 input, bf16 or f16 (a.out_f16) output, up in {2, 4} with 6*up taps, down 2 with 12 taps, no
 // bias (folded into the producer).  Sets tiles/cblocks itself.  Returns IC2_E_UNSUPPORTED when the

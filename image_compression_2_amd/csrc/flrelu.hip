@@ -317,7 +317,7 @@ static float f16_step(float r, bool up) {  // the next f16 value above / below r
   b = (up != neg) ? b + 1 : b - 1;
   return (float)__builtin_bit_cast(_Float16, b);
 }
-static void f16_round_taps(const float* exact, float* out, int n, int stride_groups) {
+void f16_round_taps(const float* exact, float* out, int n, int stride_groups) {
   // out[t] = f16-representable, per group (t mod stride_groups) sum error minimal
   for (int t = 0; t < n; ++t) out[t] = f16_nearest(exact[t]);
   for (int g = 0; g < stride_groups; ++g) {
@@ -404,6 +404,15 @@ static int flrelu_common(const void* x, void* y, int dtype_in, int dtype_out, bo
     f16_round_taps(gdg, a.gdg, fd_taps, 1);
     a.slope = slope;
     a.lim = clamp >= 0.f ? clamp / gain : INFINITY;
+    for (int t = 0; t < 24; ++t) a.guh[t] = 0.f;
+    for (int t = 0; t < 12; ++t) a.gdgl[t] = 0.f;
+    if (clamp >= 0.f) {  // the clamp-split kernels' horizontal passes: u / lim and the gain * lim down taps
+      float guh[24] = {}, gdgl[12] = {};
+      for (int t = 0; t < fu_taps; ++t) guh[t] = gu[t] / a.lim;
+      for (int t = 0; t < fd_taps; ++t) gdgl[t] = gdg[t] * a.lim;
+      f16_round_taps(guh, a.guh, fu_taps, up);
+      f16_round_taps(gdgl, a.gdgl, fd_taps, 1);
+    }
     if (flrelu_mfma_launch(a, dtype_in == IC2_F16, up, down, fu_taps, fd_taps, dx, n, s) == IC2_OK) {
       IC2_CHECK_LAUNCH(name);
       return IC2_OK;

@@ -20,6 +20,7 @@
 //   stage C  per column: vertical down-by-up FIR -> gx (f32) -> global
 // f32 arithmetic throughout (the gradient is returned in f32 whatever the forward's storage dtype).
 #include "common.h"
+#include "flrelu.h"
 
 #include <cstdlib>
 
@@ -28,7 +29,7 @@ namespace ic2 {
 int flrelu_bwd_mfma_launch(const void* x, const void* gout, void* gx, const float* oscale, const float* bias,
                            float* ydot, int64_t ydot_floats, int n, int c_p, int in_h, int in_w, int out_h, int out_w,
                            const float* gu, const float* gd, int up, int p0, float gain, float slope, float lim,
-                           hipStream_t s);
+                           bool grad_f16, hipStream_t s);
 
 typedef float bf2v __attribute__((ext_vector_type(2)));
 typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
@@ -309,7 +310,8 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
   IC2_CHECK_ARG(x && gout && gx && fu && fd, "flrelu_bwd_nhwc: null pointer");
   IC2_CHECK_ARG(n > 0 && c_p > 0 && in_h > 0 && in_w > 0, "flrelu_bwd_nhwc: bad geometry");
   IC2_CHECK_ARG(x_dtype == IC2_F32 || x_dtype == IC2_F16, "flrelu_bwd_nhwc: x must be f32 or f16");
-  IC2_CHECK_ARG(g_dtype == IC2_F32 || g_dtype == IC2_BF16, "flrelu_bwd_nhwc: gout must be f32 or bf16");
+  IC2_CHECK_ARG(g_dtype == IC2_F32 || g_dtype == IC2_BF16 || g_dtype == IC2_F16,
+                "flrelu_bwd_nhwc: gout must be f32, bf16 or f16");
   const int ew = (in_w * up + (px0 + px1) - (fu_taps - 1) - (fd_taps - 1) + (down - 1)) / down;
   const int eh = (in_h * up + (py0 + py1) - (fu_taps - 1) - (fd_taps - 1) + (down - 1)) / down;
   IC2_CHECK_ARG(out_h == eh && out_w == ew && out_h > 0, "flrelu_bwd_nhwc: output %dx%d, expected %dx%d", out_h, out_w,
@@ -323,7 +325,11 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
               up, down, fu_taps, fd_taps);
     return IC2_E_UNSUPPORTED;
   }
-  IC2_CHECK_ARG(gx_dtype == IC2_F32 || gx_dtype == IC2_BF16, "flrelu_bwd_nhwc: gx must be f32 or bf16");
+  IC2_CHECK_ARG(gx_dtype == IC2_F32 || gx_dtype == IC2_BF16 || gx_dtype == IC2_F16,
+                "flrelu_bwd_nhwc: gx must be f32, bf16 or f16");
+  // f16 gradients (the f16 training path, loss-scaled): the MFMA kernel's f16-operand instance only
+  IC2_CHECK_ARG((g_dtype == IC2_F16) == (gx_dtype == IC2_F16) && (g_dtype != IC2_F16 || x_dtype == IC2_F16),
+                "flrelu_bwd_nhwc: f16 gradients need f16 x, f16 gout and f16 gx");
   FlrBwdArgs a;
   a.x = x; a.gout = gout; a.gx = gx;
   a.oscale = oscale; a.bias = bias; a.ydot = ydot; a.out_bf16 = gx_dtype == IC2_BF16;
@@ -336,16 +342,22 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
   // the bf16 training path (f16 x, bf16 gout and gx): the MFMA kernel (flrelu_bwd_mfma.hip) unless knob
   // IC2_FLRB_MFMA=0; ydot from the stored gx there
   static const bool mfma = knob("IC2_FLRB_MFMA", 1) != 0;
-  if (mfma && x_dtype == IC2_F16 && g_dtype == IC2_BF16 && gx_dtype == IC2_BF16) {
+  const bool gf16 = g_dtype == IC2_F16;
+  if ((mfma || gf16) && x_dtype == IC2_F16 && ((g_dtype == IC2_BF16 && gx_dtype == IC2_BF16) || gf16)) {
     const int64_t need = (int64_t)n * ceil_div(in_h, 16) * ceil_div(in_w, 16) * c_p;
     IC2_CHECK_ARG(ydot == nullptr || ydot_floats >= need, "flrelu_bwd_nhwc: ydot needs %lld floats", (long long)need);
-    const int rc = flrelu_bwd_mfma_launch(x, gout, gx, oscale, bias, ydot, need, n, c_p, in_h, in_w, out_h, out_w, a.gu,
-                                          a.gd, up, px0, gain, slope, a.lim, as_stream(stream));
+    // U is recomputed with the forward's f16 taps: the same joint per-phase rounding, so the lrelu side
+    // and the clamp are decided on the forward's vertical operands
+    float gur[24] = {}, gdr[12] = {};
+    f16_round_taps(a.gu, gur, fu_taps, up);
+    f16_round_taps(a.gd, gdr, fd_taps, 1);
+    const int rc = flrelu_bwd_mfma_launch(x, gout, gx, oscale, bias, ydot, need, n, c_p, in_h, in_w, out_h, out_w, gur,
+                                          gdr, up, px0, gain, slope, a.lim, gf16, as_stream(stream));
     if (rc == IC2_OK) {
       IC2_CHECK_LAUNCH("flrelu_bwd_nhwc (mfma)");
       return IC2_OK;
     }
-    if (rc != IC2_E_UNSUPPORTED) return rc;
+    if (rc != IC2_E_UNSUPPORTED || gf16) return rc;
   }
   // gout phase: R = td - 1 - ph with ph = (-(p0 - tu + 1 - td + 1)) mod down (up % down == 0: same for every tile)
   const int q = px0 - fu_taps + 1 - fd_taps + 1;

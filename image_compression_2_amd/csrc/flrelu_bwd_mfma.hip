@@ -13,8 +13,10 @@
 //                GU = GA * act'(U) on the accumulators;   P^T[c][jx]   = GU^T[c][kx] . Gu      (GU is the A operand)
 //   vertical:    GX^T[c][jy] += P^T[c][ky] . Gu           (per gx column, P from LDS)
 // U is recomputed exactly as the forward computes it (f16 operands, f16 taps, V rounded to f16), so the lrelu / clamp
-// decisions are the forward's; the gradient passes run on bf16 operands (the training path's gradient dtype: the
-// range of f16 does not hold dL/dout) with f32 accumulation.
+// decisions are the forward's; the gradient passes run on the gradient dtype's operands with f32 accumulation: bf16
+// (the bf16 training path: the range of f16 does not hold an unscaled dL/dout) or f16 (GF16: the f16 training path,
+// whose loss is scaled as the reference's GradScaler does, stylegan3_hvae_full.py:487,693-696; stores overflow to
+// inf, never saturate, so the scaler sees an overflow).
 //
 // A work item is a strip: one sample x TJX gx columns x 16 channels x a run of 16-row tiles, walked top to bottom
 // like the forward's strip kernel.  Tile t needs grid rows 16 U t - 6 U + 1 + p0 ... (21 U of them): NBT blocks of 16
@@ -73,12 +75,21 @@ struct FbmGeom {
   static_assert(2 * GG_DW + 7 * GP + 8 * NW * ((NOX + NW - 1) / NW) <= GR_DW, "gout ring bounds");
 };
 
-__device__ __forceinline__ uint32_t fb_bf2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
-__device__ __forceinline__ fb_s4 fb_bf4(float a, float b, float c, float d) {
-  return __builtin_bit_cast(fb_s4, make_uint2(fb_bf2(a, b), fb_bf2(c, d)));
+// gradient-dtype helpers: GF16 = f16 operands (IEEE conversion: overflow -> inf), else bf16
+template <bool GF16>
+__device__ __forceinline__ uint32_t fb_g2(float a, float b) {
+  if constexpr (GF16) return fm_h2u(a, b);
+  else return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
-__device__ __forceinline__ fm_f4 fb_mfma_bf16(fb_s4 a, fb_s4 b, fm_f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+template <bool GF16>
+__device__ __forceinline__ fb_s4 fb_g4(float a, float b, float c, float d) {
+  return __builtin_bit_cast(fb_s4, make_uint2(fb_g2<GF16>(a, b), fb_g2<GF16>(c, d)));
+}
+template <bool GF16>
+__device__ __forceinline__ fm_f4 fb_mfma_g(fb_s4 a, fb_s4 b, fm_f4 c) {
+  if constexpr (GF16)
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(fm_h4, a), __builtin_bit_cast(fm_h4, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ fm_f4 fb_mfma_f16(fm_h4 a, fm_h4 b, fm_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
@@ -97,7 +108,7 @@ __device__ __forceinline__ float fb_dact(float u, float ga, float slope, float g
 #define FBM_OS_DMA 0
 #endif
 
-template <int U, int TJX>
+template <int U, int TJX, bool GF16>
 __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, int nitems, int nseg, int seg_len) {
   using G = FbmGeom<U, TJX>;
   constexpr int NW = G::NW, NT = 64 * NW, NBT = G::NBT, NBX = G::NBX, NINX = G::NINX, NOX = G::NOX, S = G::S;
@@ -217,8 +228,8 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
   // p0 + 1, the same on both axes)
   const int r0 = (a.p0 - 6 * U + 1) - 2 * o_first(a.p0 - 6 * U + 1);
   fm_h4 gmy, gmx[NBX];  // f16: vertical up B [jj][kk]; horizontal up A [kk][jj] over the clipped V window of block tt
-  fb_s4 gdy, gdx[NBX];  // bf16: vertical GA B [oo][kk]; horizontal GA A [kk][oo] over the clipped GAv window
-  fb_s4 gT[G::NG];      // bf16: h-up^T / v-up^T B [k][j] of grid block b: gu[U j + 6U - 1 - 16 b - k]
+  fb_s4 gdy, gdx[NBX];  // gradient dtype: vertical GA B [oo][kk]; horizontal GA A [kk][oo] over the clipped GAv window
+  fb_s4 gT[G::NG];      // gradient dtype: h-up^T / v-up^T B [k][j] of grid block b: gu[U j + 6U - 1 - 16 b - k]
   {
     float v[4];
 #pragma unroll
@@ -226,7 +237,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
     gmy = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = gd_t(r0 + li - 2 * (4 * g + j));
-    gdy = fb_bf4(v[0], v[1], v[2], v[3]);
+    gdy = fb_g4<GF16>(v[0], v[1], v[2], v[3]);
 #pragma unroll
     for (int tt = 0; tt < NBX; ++tt) {
       const int wv = min(16 * tt / U, NINX - 16), wo = min(8 * tt, NOX - 16);
@@ -235,13 +246,13 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
       gmx[tt] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = gd_t(r0 + 16 * tt + li - 2 * (wo + 4 * g + j));
-      gdx[tt] = fb_bf4(v[0], v[1], v[2], v[3]);
+      gdx[tt] = fb_g4<GF16>(v[0], v[1], v[2], v[3]);
     }
 #pragma unroll
     for (int b = 0; b < G::NG; ++b) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = gu_t(U * li + 6 * U - 1 - 16 * b - (4 * g + j));
-      gT[b] = fb_bf4(v[0], v[1], v[2], v[3]);
+      gT[b] = fb_g4<GF16>(v[0], v[1], v[2], v[3]);
     }
   }
   const float slope = a.slope, gain = a.gain, lim = a.lim;
@@ -300,7 +311,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
 #pragma unroll
         for (int i = 0; i < NC; ++i) vt[i] = fb_mfma_f16(__builtin_bit_cast(fm_h4, xa[i]), gmy, fm_f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int i = 0; i < NCO; ++i) at[i] = fb_mfma_bf16(ga_[i], gdy, fm_f4{0.f, 0.f, 0.f, 0.f});
+        for (int i = 0; i < NCO; ++i) at[i] = fb_mfma_g<GF16>(ga_[i], gdy, fm_f4{0.f, 0.f, 0.f, 0.f});
         __builtin_amdgcn_sched_barrier(0);
         // V overwrites P: every wave's v-up^T reads of block k-1 are done (block 0: the item-top barrier)
         if (k > 0) __syncthreads();
@@ -313,7 +324,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
 #pragma unroll
         for (int i = 0; i < NCO; ++i)
           if (i < NCO - 1 || wave + NW * i < NOX)
-            *reinterpret_cast<uint2*>(ap + i * NW * 8) = make_uint2(fb_bf2(at[i][0], at[i][1]), fb_bf2(at[i][2], at[i][3]));
+            *reinterpret_cast<uint2*>(ap + i * NW * 8) = make_uint2(fb_g2<GF16>(at[i][0], at[i][1]), fb_g2<GF16>(at[i][2], at[i][3]));
       }
       __syncthreads();  // B1: V and GAv complete; the ring groups k are dead; every wave's v-up^T of block k-1 done
       if (k == kend && has_next) load_item(w + gridDim.x);  // every ring slot is dead: the next item's first rows
@@ -333,7 +344,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
 #pragma unroll
         for (int tt = 0; tt < NBX; ++tt) {
           u[tt] = fb_mfma_f16(gmx[tt], __builtin_bit_cast(fm_h4, vb[tt]), fm_f4{0.f, 0.f, 0.f, 0.f});
-          ga[tt] = fb_mfma_bf16(gdx[tt], gb[tt], fm_f4{0.f, 0.f, 0.f, 0.f});
+          ga[tt] = fb_mfma_g<GF16>(gdx[tt], gb[tt], fm_f4{0.f, 0.f, 0.f, 0.f});
         }
         __builtin_amdgcn_sched_barrier(0);
         fm_f4 pt = fm_f4{0.f, 0.f, 0.f, 0.f};
@@ -343,14 +354,14 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
           float uu[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) uu[r] = (float)(_Float16)u[tt][r];
-          const fb_s4 gu4 = fb_bf4(fb_dact(uu[0], ga[tt][0], slope, gain, lim), fb_dact(uu[1], ga[tt][1], slope, gain, lim),
+          const fb_s4 gu4 = fb_g4<GF16>(fb_dact(uu[0], ga[tt][0], slope, gain, lim), fb_dact(uu[1], ga[tt][1], slope, gain, lim),
                                    fb_dact(uu[2], ga[tt][2], slope, gain, lim), fb_dact(uu[3], ga[tt][3], slope, gain, lim));
-          pt = fb_mfma_bf16(gu4, gT[tt], pt);
+          pt = fb_mfma_g<GF16>(gu4, gT[tt], pt);
         }
         __builtin_amdgcn_sched_barrier(0);
         // P row `row` over this wave's own V row (its reads of it above are done: LDS ops of a wave run in order)
         *reinterpret_cast<uint2*>(v_img + row * G::VP + li * G::P_XP + 2 * g) =
-            make_uint2(fb_bf2(pt[0], pt[1]), fb_bf2(pt[2], pt[3]));
+            make_uint2(fb_g2<GF16>(pt[0], pt[1]), fb_g2<GF16>(pt[2], pt[3]));
       }
       // B2: the ring groups loaded at block k-1 (for block k+1) must have landed; the stores of a tile finished at
       // block k-1 (issued after that DMA, exactly OCW) may stay in flight
@@ -374,12 +385,12 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
         __builtin_amdgcn_sched_barrier(0);
         if (t1 < nt) {
 #pragma unroll
-          for (int i = 0; i < OCW; ++i) accB[i] = fb_mfma_bf16(pa[i], gT[BB], accB[i]);
+          for (int i = 0; i < OCW; ++i) accB[i] = fb_mfma_g<GF16>(pa[i], gT[BB], accB[i]);
         }
         if constexpr (BB + U < NBT) {
           if (t1 >= 1) {
 #pragma unroll
-            for (int i = 0; i < OCW; ++i) accA[i] = fb_mfma_bf16(pa[i], gT[BB + U], accA[i]);
+            for (int i = 0; i < OCW; ++i) accA[i] = fb_mfma_g<GF16>(pa[i], gT[BB + U], accA[i]);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -392,8 +403,8 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
           for (int i = 0; i < OCW; ++i) {
             const int gxc = jx0 + wave + NW * i;
             const uint32_t off = (gy < a.in_h && gxc < a.in_w) ? (uint32_t)((gy * xsy + gxc * a.c_p + 4 * g) * 2) : FM_OOB;
-            const uint2 v = make_uint2(fb_bf2(accA[i][0] * osc[0], accA[i][1] * osc[1]),
-                                       fb_bf2(accA[i][2] * osc[2], accA[i][3] * osc[3]));
+            const uint2 v = make_uint2(fb_g2<GF16>(accA[i][0] * osc[0], accA[i][1] * osc[1]),
+                                       fb_g2<GF16>(accA[i][2] * osc[2], accA[i][3] * osc[3]));
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, off, 0, 0);
           }
         }
@@ -419,7 +430,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
   }
 }
 
-template <int U, int TJX>
+template <int U, int TJX, bool GF16>
 static void fbm_launch(FlrBwdMArgs a, int n, hipStream_t s) {
   a.tiles_x = (int)ceil_div(a.in_w, TJX);
   a.tiles_y = (int)ceil_div(a.in_h, 16);
@@ -429,7 +440,7 @@ static void fbm_launch(FlrBwdMArgs a, int n, hipStream_t s) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_bwd_mfma_kernel<U, TJX>, 512, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_bwd_mfma_kernel<U, TJX, GF16>, 512, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int64_t nstrips = (int64_t)n * a.tiles_x * a.cblocks;
@@ -438,12 +449,13 @@ static void fbm_launch(FlrBwdMArgs a, int n, hipStream_t s) {
   nseg = (int)ceil_div(a.tiles_y, seg_len);
   const int nitems = (int)(nstrips * nseg);
   const int grid = nitems < resident ? nitems : resident;
-  hipLaunchKernelGGL((flrelu_bwd_mfma_kernel<U, TJX>), dim3((unsigned)grid), dim3(512), 0, s, a, nitems, nseg, seg_len);
+  hipLaunchKernelGGL((flrelu_bwd_mfma_kernel<U, TJX, GF16>), dim3((unsigned)grid), dim3(512), 0, s, a, nitems, nseg, seg_len);
 }
 
 // per (sample, pixel chunk, channel) sums of gx * (x - bias) = dc * (x - bias) / oscale: the modulated conv's
 // d oscale numerator (as the f32 kernel's ydot) from the stored dc = gx * oscale; chunk c covers pixels
 // [c * per, (c + 1) * per)
+template <bool GF16>
 __global__ void __launch_bounds__(256) fb_ydot_kernel(const uint16_t* __restrict__ dc, const uint16_t* __restrict__ x,
                                                       const float* __restrict__ oscale, const float* __restrict__ bias,
                                                       float* __restrict__ part, int hw, int c_p, int nchunks, int per) {
@@ -475,8 +487,17 @@ __global__ void __launch_bounds__(256) fb_ydot_kernel(const uint16_t* __restrict
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const fm_h2 xh = __builtin_bit_cast(fm_h2, xw[k]);
-          acc[2 * k] += __uint_as_float(dw[k] << 16) * ((float)xh.x - b[2 * k]);
-          acc[2 * k + 1] += __uint_as_float(dw[k] & 0xffff0000u) * ((float)xh.y - b[2 * k + 1]);
+          float d0, d1;
+          if constexpr (GF16) {
+            const fm_h2 dh = __builtin_bit_cast(fm_h2, dw[k]);
+            d0 = (float)dh.x;
+            d1 = (float)dh.y;
+          } else {
+            d0 = __uint_as_float(dw[k] << 16);
+            d1 = __uint_as_float(dw[k] & 0xffff0000u);
+          }
+          acc[2 * k] += d0 * ((float)xh.x - b[2 * k]);
+          acc[2 * k + 1] += d1 * ((float)xh.y - b[2 * k + 1]);
         }
       }
     }
@@ -500,13 +521,13 @@ __global__ void __launch_bounds__(256) fb_ydot_kernel(const uint16_t* __restrict
   }
 }
 
-// The bf16 training path's FLR backward on MFMA (called by ic2_flrelu_bwd_nhwc_ex for f16 x, bf16 gout and bf16 gx;
-// returns IC2_E_UNSUPPORTED for the geometries it has no instance for).  ydot (optional): n x nchunks x c_p partial
+// The training path's FLR backward on MFMA (called by ic2_flrelu_bwd_nhwc_ex for f16 x and bf16 gout / gx, or f16
+// gout / gx with grad_f16; returns IC2_E_UNSUPPORTED for the geometries it has no instance for).  ydot (optional): n x nchunks x c_p partial
 // sums of dc * (x - bias), nchunks = ydot_floats / (n c_p).
 int flrelu_bwd_mfma_launch(const void* x, const void* gout, void* gx, const float* oscale, const float* bias,
                            float* ydot, int64_t ydot_floats, int n, int c_p, int in_h, int in_w, int out_h, int out_w,
                            const float* gu, const float* gd, int up, int p0, float gain, float slope, float lim,
-                           hipStream_t s) {
+                           bool grad_f16, hipStream_t s) {
   if (c_p % 16 != 0 || (up != 2 && up != 4)) return IC2_E_UNSUPPORTED;
   if ((int64_t)in_h * in_w * c_p * 2 >= (int64_t)FM_OOB || (int64_t)out_h * out_w * c_p * 2 >= (int64_t)FM_OOB)
     return IC2_E_UNSUPPORTED;
@@ -517,15 +538,25 @@ int flrelu_bwd_mfma_launch(const void* x, const void* gout, void* gx, const floa
   a.slope = slope; a.gain = gain; a.lim = lim;
   for (int t = 0; t < 24; ++t) a.gu[t] = gu[t];
   for (int t = 0; t < 12; ++t) a.gd[t] = gd[t];
-  if (up == 2) fbm_launch<2, 16>(a, n, s);
-  else fbm_launch<4, 8>(a, n, s);
+  if (grad_f16) {
+    if (up == 2) fbm_launch<2, 16, true>(a, n, s);
+    else fbm_launch<4, 8, true>(a, n, s);
+  } else {
+    if (up == 2) fbm_launch<2, 16, false>(a, n, s);
+    else fbm_launch<4, 8, false>(a, n, s);
+  }
   if (ydot) {
     const int nchunks = (int)(ydot_floats / ((int64_t)n * c_p));
     if (nchunks < 1) return IC2_E_INVALID;
     const int hw = in_h * in_w, per = (int)ceil_div(hw, nchunks);
-    hipLaunchKernelGGL(fb_ydot_kernel, dim3((unsigned)nchunks, (unsigned)n), dim3(256), 0, s,
-                       reinterpret_cast<const uint16_t*>(gx), reinterpret_cast<const uint16_t*>(x), oscale, bias, ydot, hw, c_p,
-                       nchunks, per);
+    if (grad_f16)
+      hipLaunchKernelGGL(fb_ydot_kernel<true>, dim3((unsigned)nchunks, (unsigned)n), dim3(256), 0, s,
+                         reinterpret_cast<const uint16_t*>(gx), reinterpret_cast<const uint16_t*>(x), oscale, bias, ydot,
+                         hw, c_p, nchunks, per);
+    else
+      hipLaunchKernelGGL(fb_ydot_kernel<false>, dim3((unsigned)nchunks, (unsigned)n), dim3(256), 0, s,
+                         reinterpret_cast<const uint16_t*>(gx), reinterpret_cast<const uint16_t*>(x), oscale, bias, ydot,
+                         hw, c_p, nchunks, per);
   }
   return IC2_OK;
 }

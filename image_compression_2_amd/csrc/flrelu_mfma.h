@@ -14,6 +14,9 @@ typedef float fm_f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
 
 constexpr int FM_TAPS = 276;
+// the wide / strip kernels' table also holds the clamp-split horizontal taps: guh at [328, 352), gdgl at [428, 440)
+// (zero guards around each: the tap reads reach 15 below and 63 above gu's base, 30 below and 47 above gdg's)
+constexpr int FM_TAPS_CL = 476;
 constexpr uint32_t FM_OOB = 0x7ffffff0u;  // buffer num_records = the zero-answer offset (per-sample image < 2 GiB)
 
 

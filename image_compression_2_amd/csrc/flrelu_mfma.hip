@@ -455,7 +455,7 @@ struct FmGeom2 {
   static constexpr int D_XP = 10;
   static constexpr int D_PITCH = TOX * D_XP + 8;
   static constexpr int D_DW = 16 * D_PITCH;
-  static constexpr int DT_DW = D_DW > FM_TAPS ? D_DW : FM_TAPS;  // D image, aliased by the tap table
+  static constexpr int DT_DW = D_DW > FM_TAPS_CL ? D_DW : FM_TAPS_CL;  // D image, aliased by the tap table
   static constexpr int LDS_DW = IN_DW + V_DW + DT_DW + 16;       // + the tile's 16 post-scale floats
   static_assert(NINX % 2 == 1 && NINY % 2 == 1 && NINY >= 16, "input image sides must be odd and cover a window");
   static_assert(NBX == 2 * NOB + 1, "horizontal down: output block ob reads grid blocks 2ob .. 2ob+2");
@@ -479,11 +479,13 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
 
-  for (int i = tid; i < FM_TAPS; i += NT) {
+  for (int i = tid; i < FM_TAPS_CL; i += NT) {
     float v = 0.f;
     if (i >= 48 && i < 72) v = a.gu[i - 48];
     else if (i >= 148 && i < 160) v = a.gd[i - 148];
     else if (i >= 228 && i < 240) v = a.gdg[i - 228];
+    else if (i >= 328 && i < 352) v = a.guh[i - 328];
+    else if (i >= 428 && i < 440) v = a.gdgl[i - 428];
     taps[i] = v;
   }
 
@@ -569,13 +571,13 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
     for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
     gmy[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
-  const float inv_lim = CL ? 1.f / a.lim : 1.f;  // CL: the horizontal up pass yields u / lim
+  // CL: the horizontal up pass yields u / lim (host-scaled taps guh), the down taps carry lim (gdgl)
 #pragma unroll
   for (int t = 0; t < NBX; ++t) {
     const int w0 = fm_win<U, DELTA, NINX>(16 * t);
     float v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)] * inv_lim;
+    for (int j = 0; j < 4; ++j) v[j] = taps[(CL ? 328 : 48) + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
     gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
   // horizontal down matrices over kx blocks (K = 32 per MFMA).  Plain: [b0; b1], [b2; 0] against (u0, u1),
@@ -583,8 +585,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma2_kernel(FlrArgs 
   // one register tuple, shared as-is by the two output blocks that read it (no operand copies)
   fm_h8 gdh01, gdh2, gdq[3];
   {
-    const float sc = CL ? a.lim : 1.f;
-    auto tap = [&](int blk, int j) { return taps[228 + 16 * blk + 4 * g + j - 2 * li] * sc; };
+    auto tap = [&](int blk, int j) { return taps[(CL ? 428 : 228) + 16 * blk + 4 * g + j - 2 * li]; };
     float v[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -815,11 +816,13 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
   // this lane's row in a vertical-up window, as (ring group offset, row in group)
   const int qoff = (4 * g + tq) / S, roff = (4 * g + tq) % S;
 
-  for (int i = tid; i < FM_TAPS; i += NT) {
+  for (int i = tid; i < FM_TAPS_CL; i += NT) {
     float v = 0.f;
     if (i >= 48 && i < 72) v = a.gu[i - 48];
     else if (i >= 148 && i < 160) v = a.gd[i - 148];
     else if (i >= 228 && i < 240) v = a.gdg[i - 228];
+    else if (i >= 328 && i < 352) v = a.guh[i - 328];
+    else if (i >= 428 && i < 440) v = a.gdgl[i - 428];
     taps[i] = v;
   }
 
@@ -893,19 +896,17 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
     for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (4 * g + j) + DELTA - li];
     gmy = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
-  const float inv_lim = CL ? 1.f / a.lim : 1.f;
 #pragma unroll
   for (int t = 0; t < NBX; ++t) {
     const int w0 = fm_win<U, DELTA, NINX>(16 * t);
     float v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = taps[48 + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)] * inv_lim;
+    for (int j = 0; j < 4; ++j) v[j] = taps[(CL ? 328 : 48) + U * (w0 + 4 * g + j) + DELTA - (16 * t + li)];
     gmx[t] = fm_h4_of(fm_pack4(v[0], v[1], v[2], v[3]));
   }
   fm_h8 gdh01, gdh2, gdq[3];
   {
-    const float sc = CL ? a.lim : 1.f;
-    auto tap = [&](int blk, int j) { return taps[228 + 16 * blk + 4 * g + j - 2 * li] * sc; };
+    auto tap = [&](int blk, int j) { return taps[(CL ? 428 : 228) + 16 * blk + 4 * g + j - 2 * li]; };
     float v[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -556,6 +556,7 @@ class SynthesisNetwork(torch.nn.Module):
         self.num_fp16_res = num_fp16_res
         self.precision = precision
         nv.torch_dtype(precision)
+        self.train_f16 = False   # autograd path in f16 (loss-scaled training, training.train_step(scaler=...))
 
         last_cutoff = self.img_resolution / 2
         last_stopband = last_cutoff * last_stopband_rel
@@ -598,8 +599,10 @@ class SynthesisNetwork(torch.nn.Module):
         assert ws.ndim == 3 and ws.shape[1] == self.num_ws and ws.shape[2] == self.w_dim, ws.shape
         dt = torch.float32 if force_fp32 else nv.torch_dtype(self.precision)
         if _train_mode(self, ws):
-            # 'f16' is an inference precision: the autograd path trains in bf16 (as the encoder's 'bf16x3')
-            return self.forward_train(ws, torch.bfloat16 if dt == torch.float16 else dt)
+            # 'f16' trains in f16 only when the caller scales its loss (train_f16: the reference's fp16 autocast +
+            # GradScaler, stylegan3_hvae_full.py:487,693-696; unscaled gradients underflow f16), else in bf16
+            tdt = dt if dt != torch.float16 or self.train_f16 else torch.bfloat16
+            return self.forward_train(ws, tdt)
         ws_in = ws
         ws = ws.to(torch.float32).contiguous()
         nv.require_gpu(ws)

@@ -178,6 +178,15 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
         nv.call("ic2_group_norm_stats", nv.ptr(y), nv.F32, ya.n, ya.h * ya.w, ya.c_p, ya.c, norm.num_groups,
                 float(norm.eps), nv.ptr(stats), stream)
         return ya, stats
+    if dt == torch.float16:
+        # f16 (the training precision's inference forward): the conv, then the separate statistics pass (the fused
+        # statistics epilogue is bf16 halo-conv code)
+        ya = _conv(conv, x, dt, cache, stream)
+        nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
+        stats = torch.empty([nfl], dtype=torch.float32, device=ya.t.device)
+        nv.call("ic2_group_norm_stats", nv.ptr(ya.t), nv.F16, ya.n, ya.h * ya.w, ya.c_p, ya.c, norm.num_groups,
+                float(norm.eps), nv.ptr(stats), stream)
+        return ya, stats
     dc = nv.dtype_code(dt)
     y = torch.empty([x.n, ho, wo, cout_p], dtype=dt, device=x.t.device)
     nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", dc, x.n, x.h, x.w, x.c_p, cout_p, kh, kw, pad, norm.num_groups))
@@ -272,7 +281,8 @@ class HVAE_VGG_Encoder(nn.Module):
         """Extensions (not in the reference), both opt-in:
         precision: 'fp32' (parity, exact-f32 MFMA), 'bf16' (bf16 storage and MFMA), 'bf16x3' (split bf16: three bf16
             MFMA terms per product, f32 storage -- latents at fp32 level, the 8-bit indices of the fp32 reference;
-            DESIGN.md (c)).
+            DESIGN.md (c)), 'f16' (f16 storage and MFMA: the training precision of BASELINE config 5, used with a
+            loss scaler as the reference's fp16 autocast + GradScaler, stylegan3_hvae_full.py:487,669,693-696).
         fix_fine_projector: the reference builds the fine projector's fc1 for 64 inputs, receives 128 and re-creates
             fc1 with fresh random weights on every call (:225-230, SURVEY.md 5 bug 1).  True builds fc1 for the
             pooled width once, right after the reference's construction (so every other weight is still drawn as the

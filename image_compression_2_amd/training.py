@@ -15,8 +15,11 @@ Deviations, all explicit:
   * LPIPS(net='vgg') needs pretrained VGG weights that cannot be fetched here (no network): ``percep`` is a
     caller-supplied callable; with ``percep=None`` a non-zero ``perceptual_weight`` raises.
   * Without fp16 the reference runs its forward under ``torch.no_grad()`` (:668) and its loss.backward()
-    then fails; this step always builds the graph (the reference's fp16 branch: autocast + GradScaler; here
-    ``precision='bf16'`` on the modules, which needs no loss scaling).
+    then fails; this step always builds the graph.  Precision: ``precision='bf16'`` on the modules (no loss
+    scaling needed), or the reference's fp16 branch (:487, :669, :693-696: autocast + GradScaler) as f16
+    modules (encoder 'f16', generator 'f16' with ``synthesis.train_f16``) plus a ``torch.amp.GradScaler`` passed as
+    ``scaler``: the loss is scaled before backward, the step is skipped and the scale backed off when a gradient
+    overflowed (the f16 kernels store gradients IEEE, so an overflow arrives as inf), as the reference's scaler does.
   * Multi-GPU: data parallel, one process per GPU, gradients averaged by distributed.allreduce_gradients.  The
     fine projector's fc1, which the reference re-creates from the CPU generator on every call (:225-230), is
     broadcast from rank 0 after each re-creation, so every rank runs -- and averages the gradients of -- the same
@@ -43,14 +46,25 @@ def make_optimizer(encoder, lr=1e-4):
     return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), fused=fused or None)
 
 
+def make_f16(compressor):
+    """The reference's fp16 training (autocast + GradScaler, :487, :669, :693-696) on this path: f16 activations and
+    MFMA operands in the encoder and the frozen synthesis (gradients too), f32 master weights and Adam state.
+    -> the GradScaler to pass to train_step (torch's: init scale 2^16, growth 2 every 2000 clean steps, backoff 0.5)."""
+    compressor.encoder.set_precision("f16")
+    compressor.generator.set_precision("f16")
+    compressor.generator.synthesis.train_f16 = True
+    return torch.amp.GradScaler("cuda")
+
+
 def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_weight=0.8, kl_weight=0.01,
-               percep=None, second_encoder_pass=True, sync_gradients=None):
+               percep=None, second_encoder_pass=True, sync_gradients=None, scaler=None):
     """One optimisation step; returns the four losses as 0-d device tensors (no host sync).
 
     ``w_avg``: G.mapping.w_avg shaped [1, 1, w_dim] (ref :626).  ``second_encoder_pass=False`` reuses the
     first pass's means / logvars for the KL term (identical values unless the projector's fc1 quirk redraws
     fc1, ref :225-230) and skips one encoder forward.  ``sync_gradients``: world size for the data-parallel
-    gradient average (default: the initialised process group's)."""
+    gradient average (default: the initialised process group's).  ``scaler``: a torch.amp.GradScaler for f16 training
+    (make_f16): scaled backward, then unscale + overflow check + step + scale update, as the reference's :693-696."""
     if percep is None and perceptual_weight != 0:
         raise ValueError("perceptual_weight != 0 needs a perceptual loss callable (the reference's LPIPS(net='vgg') "
                          "weights are not available offline): pass percep=... or perceptual_weight=0")
@@ -64,14 +78,14 @@ def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_
             proj.fc1_hook = icd.broadcast_params
     try:
         return _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight,
-                           percep, second_encoder_pass, sync_gradients)
+                           percep, second_encoder_pass, sync_gradients, scaler)
     finally:
         for proj in projectors:
             proj.fc1_hook = None
 
 
 def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight, percep,
-                second_encoder_pass, sync_gradients):
+                second_encoder_pass, sync_gradients, scaler=None):
     with torch.enable_grad():
         if second_encoder_pass:
             reconstructed, _ = compressor(images)
@@ -86,8 +100,13 @@ def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perce
         perceptual = percep(images, reconstructed).mean() if percep is not None else rec_loss.new_zeros(())
         kl = kl_divergence(means, logvars, w_avg)
         loss = rec_weight * rec_loss + perceptual_weight * perceptual + kl_weight * kl
-        loss.backward()
+        (scaler.scale(loss) if scaler is not None else loss).backward()
+    # the average of scaled gradients is the scaled average: the scaler unscales after the all_reduce
     icd.allreduce_gradients(list(encoder.parameters()), sync_gradients)
-    optimizer.step()
+    if scaler is not None:
+        scaler.step(optimizer)
+        scaler.update()
+    else:
+        optimizer.step()
     return {"rec_loss": rec_loss.detach(), "kl_loss": kl.detach(), "perceptual_loss": perceptual.detach(),
             "total_loss": loss.detach()}

@@ -24,7 +24,7 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
-def _grad_check(cuda, kw, x, precision, tol, seed=7):
+def _grad_check(cuda, kw, x, precision, tol, seed=7, loss_scale=1.0):
     torch.manual_seed(seed)
     enc = ic2.HVAE_VGG_Encoder(precision=precision, **kw).to(cuda)
     xg = x.clone().to(cuda).requires_grad_(True)
@@ -33,7 +33,7 @@ def _grad_check(cuda, kw, x, precision, tol, seed=7):
     g = torch.Generator().manual_seed(3)
     r = [torch.randn(t.shape, generator=g) for t in (w, m, lv)]
     loss = sum((t * ri.to(cuda)).sum() for t, ri in zip((w, m, lv), r))
-    loss.backward()
+    (loss * loss_scale).backward()   # f16: scaled as the reference's GradScaler scales its loss
     # oracle: same weights (fp64 leaves), the fc1 this call drew, the eps this call drew
     named = dict(enc.named_parameters())
     sd = {k: v.detach().cpu().double().requires_grad_(True) for k, v in named.items()}
@@ -57,7 +57,7 @@ def _grad_check(cuda, kw, x, precision, tol, seed=7):
     gmax = max(b.norm().item() for _, b in pairs.values())
     worst = {}
     for k, (a, b) in pairs.items():
-        a = a.detach().double().cpu()
+        a = a.detach().double().cpu() / loss_scale
         if b.norm().item() < 1e-8 * gmax:
             # exactly-zero true gradient (conv bias before a one-channel GroupNorm group): rounding noise only
             assert a.norm().item() < 1e-4 * gmax, k
@@ -81,6 +81,15 @@ def test_encoder_backward_full_fp32(cuda):
     _grad_check(cuda, dict(img_resolution=1024), x, "fp32", 1e-3, seed=0)
 
 
+def test_encoder_backward_full_f16(cuda):
+    """f16 mode, BASELINE config 5's precision (the reference's fp16 autocast + GradScaler, stylegan3_hvae_full.py:
+    487,669,693-696): f16 activations, gradients and MFMA operands, f32 accumulation and weight gradients, the loss
+    scaled by 2^10 before backward and the gradients unscaled after, as the scaler does.  11-bit significands: the
+    same GroupNorm amplification as bf16 (below) at ~1/8 of its error."""
+    x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    _grad_check(cuda, dict(img_resolution=1024), x, "f16", 0.05, seed=0, loss_scale=1024.0)
+
+
 def test_encoder_backward_full_bf16(cuda):
     """bf16 mode (activations, dy and MFMA operands in bf16; f32 accumulation and weight gradients).  The
     GroupNorm backward of the 8^2 .. 2^2 blocks (16 channels x <= 64 pixels per group) amplifies the bf16
@@ -92,7 +101,7 @@ def test_encoder_backward_full_bf16(cuda):
 
 @pytest.mark.parametrize("cin,cout,size,pad,n", [(3, 32, 17, 1, 2), (32, 64, 20, 1, 3), (64, 96, 9, 1, 2),
                                                  (128, 32, 11, 2, 1), (96, 128, 13, 0, 2)])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_conv_backward_kernels(cuda, cin, cout, size, pad, n, dtype):
     """Conv2dNHWC backward (dx: the implicit GEMM on flipped / transposed weights; dW: ic2_conv_wgrad with the
     32-pixel K chunks split over workgroups; db) against torch autograd in fp64 on the same (rounded) operands."""
@@ -109,10 +118,10 @@ def test_conv_backward_kernels(cuda, cin, cout, size, pad, n, dtype):
         dyd = F.pad(dy.permute(0, 2, 3, 1), (0, cout_p - cout)).to(cuda, dtype)
         y.backward(dyd)
     xr = x.to(dtype).double().requires_grad_(True)
-    wr = w.to(dtype).double().requires_grad_(True) if dtype == torch.bfloat16 else w.double().requires_grad_(True)
+    wr = w.to(dtype).double().requires_grad_(True) if dtype != torch.float32 else w.double().requires_grad_(True)
     br = b.double().requires_grad_(True)
     F.conv2d(xr, wr, br, padding=pad).backward(dy.to(dtype).double())
-    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 3e-3}[dtype]
     dx = xd.grad.float().cpu()[..., :cin].permute(0, 3, 1, 2)
     assert _rel(dx, xr.grad) < tol
     assert xd.grad.float()[..., cin:].abs().max().item() == 0.0 if cin < cin_p else True
@@ -123,7 +132,7 @@ def test_conv_backward_kernels(cuda, cin, cout, size, pad, n, dtype):
 @pytest.mark.parametrize("n,c,groups,h,w,pool", [(2, 64, 32, 6, 8, True), (3, 32, 32, 9, 7, False),
                                                  (2, 128, 32, 5, 5, True), (1, 512, 32, 2, 2, True),
                                                  (2, 96, 32, 33, 17, False)])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
     g = torch.Generator().manual_seed(c + h)
     y = torch.randn(n, c, h, w, generator=g) * 2 + 0.3
@@ -142,7 +151,7 @@ def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
     if pool:
         o = F.avg_pool2d(o, 2, 2)
     o.backward(dout.to(dtype).double().permute(0, 3, 1, 2))
-    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    tol = {torch.float32: 1e-4, torch.bfloat16: 3e-2, torch.float16: 4e-3}[dtype]
     assert _rel(yd.grad.float().cpu()[..., :c].permute(0, 3, 1, 2), yr.grad) < tol
     assert _rel(gd.grad, gr.grad) < tol and _rel(bd.grad, br.grad) < tol
 
@@ -311,7 +320,7 @@ def _oracle_synthesis_grad(sd, ws, r):
     return _ORACLE_GRAD[key]
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 0.12)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 0.12), ("f16", 0.03)])
 def test_synthesis_network_gradient_wrt_ws(cuda, gen256_frozen, precision, tol):
     """dL/dws through the whole frozen SG3-T-256 synthesis (input, 14 layers, ToRGB, output scale) against
     torch.autograd through the oracle in fp64; the autograd forward equals the inference forward."""
@@ -319,6 +328,9 @@ def test_synthesis_network_gradient_wrt_ws(cuda, gen256_frozen, precision, tol):
     G = gen256_frozen
     ws = torch.randn(2, 16, 512, generator=torch.Generator().manual_seed(3)) * 0.7
     G.set_precision(precision)
+    # f16: the f16 training path (synthesis.train_f16), the loss scaled by 2^12 as a GradScaler would
+    scale = 4096.0 if precision == "f16" else 1.0
+    G.synthesis.train_f16 = precision == "f16"
     try:
         with torch.no_grad():
             inf = G.synthesis(ws.to(cuda))
@@ -327,15 +339,17 @@ def test_synthesis_network_gradient_wrt_ws(cuda, gen256_frozen, precision, tol):
         assert img.grad_fn is not None and img.shape == (2, 3, 256, 256)
         d_fwd = (img.detach() - inf).abs().max().item()
         r = torch.randn(img.shape, generator=torch.Generator().manual_seed(6))
-        (img * r.to(cuda)).sum().backward()
+        (img * r.to(cuda) * scale).sum().backward()
+        wd.grad /= scale
     finally:
         G.set_precision("fp32")
+        G.synthesis.train_f16 = False
     ref_grad = _oracle_synthesis_grad(sd, ws, r)
     e = _rel(wd.grad, ref_grad)
     per_ws = [_rel(wd.grad[:, i], ref_grad[:, i]) for i in range(16)]
     print(f"[synthesis-{precision}] rel grad error {e:.2e}; per ws {[round(v, 5) for v in per_ws]}; "
           f"|train fwd - inference fwd| {d_fwd:.2e}")
-    assert d_fwd < (1e-4 if precision == "fp32" else 2e-2)
+    assert d_fwd < {"fp32": 1e-4, "bf16": 2e-2, "f16": 4e-3}[precision]
     assert e < tol
 
 
@@ -414,6 +428,52 @@ def test_train_step_updates_encoder(cuda, gen256_frozen, second_pass):
     assert all(p.grad is None for p in gen256_frozen.parameters())
 
 
+def test_train_step_f16_loss_scaler(cuda, gen256_frozen):
+    """BASELINE config 5's fp16 step (the reference's autocast + GradScaler, stylegan3_hvae_full.py:487,669,693-696):
+    training.make_f16 + train_step(scaler=...).  The step's unscaled gradients agree with the fp32 step's on the same
+    batch (f16 operands: a few 1e-2 relative in the worst tensor), the scale stays at 2^16 (no overflow on a clean
+    step) and the parameters move; an injected overflow makes the scaler skip the step and halve its scale."""
+    x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(cuda)
+    w_avg = gen256_frozen.mapping.w_avg.view(1, 1, -1)
+    grads = {}
+    for prec in ("fp32", "f16"):
+        torch.manual_seed(0)
+        enc = ic2.HVAE_VGG_Encoder(**ENC64).to(cuda)
+        comp = ic2.StyleGAN3Compressor(enc, gen256_frozen, training_resolution=64)
+        opt = ict.make_optimizer(enc, lr=1e-4)
+        scaler = ict.make_f16(comp) if prec == "f16" else None
+        before = {k: v.detach().clone() for k, v in enc.named_parameters()}
+        try:
+            torch.manual_seed(3)
+            out = ict.train_step(comp, x, opt, w_avg, perceptual_weight=0.0, scaler=scaler)
+        finally:
+            gen256_frozen.set_precision("fp32")
+            gen256_frozen.synthesis.train_f16 = False
+        assert all(np.isfinite(v.item()) for v in out.values())
+        # a fused optimizer takes the scale into its own kernel (GradScaler leaves .grad scaled); otherwise the scaler
+        # unscaled .grad in place
+        unscale = 65536.0 if scaler is not None and getattr(opt, "_step_supports_amp_scaling", False) else 1.0
+        grads[prec] = {k: v.grad.detach().clone() / unscale for k, v in enc.named_parameters() if v.grad is not None}
+        changed = [k for k, v in enc.named_parameters() if not torch.equal(v.detach(), before[k])]
+        assert len(changed) >= len(before) // 2, changed
+        if scaler is not None:
+            assert scaler.get_scale() == 65536.0
+            # an overflowed gradient: the step is skipped and the scale halved
+            p0 = next(enc.parameters())
+            snap = {k: v.detach().clone() for k, v in enc.named_parameters()}
+            opt.zero_grad()
+            loss = (enc(x)[1].float().sum() * 0 + p0.sum() * float("inf"))
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+            assert scaler.get_scale() == 32768.0
+            assert all(torch.equal(v.detach(), snap[k]) for k, v in enc.named_parameters())
+    worst = max(_rel(grads["f16"][k], grads["fp32"][k]) for k in grads["fp32"]
+                if grads["fp32"][k].norm() > 1e-6 * max(g.norm() for g in grads["fp32"].values()))
+    print(f"[train-step f16 vs fp32] worst relative gradient difference {worst:.2e}")
+    assert worst < 0.1
+
+
 @pytest.mark.parametrize("li", [2, 5, 9, 12])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_flrelu_backward_kernel(cuda, gen256_frozen, li, mode):
@@ -447,8 +507,8 @@ def test_flrelu_backward_kernel(cuda, gen256_frozen, li, mode):
 
 
 @pytest.mark.parametrize("li", [2, 3, 5, 9, 10, 12])
-@pytest.mark.parametrize("gscale", [1.0, 1e-7])
-def test_flrelu_backward_mfma_kernel(cuda, gen256_frozen, li, gscale):
+@pytest.mark.parametrize("gscale,gdt", [(1.0, "bf16"), (1e-7, "bf16"), (1.0, "f16"), (1e3, "f16")])
+def test_flrelu_backward_mfma_kernel(cuda, gen256_frozen, li, gscale, gdt):
     """The bf16 training path's FLR backward on MFMA (flrelu_bwd_mfma.hip: f16 x, bf16 gout, bf16 gx * oscale, the
     ydot partials of d oscale) on the SG3-T-256 layer geometries (up 2: L2, L9, L12; up 4: L3, L5, L10), against
     autograd through the oracle's filtered_lrelu in fp64 on the same stored operands.  Bound: the bf16 operands of
@@ -465,17 +525,18 @@ def test_flrelu_backward_mfma_kernel(cuda, gen256_frozen, li, gscale):
     y = torch.randn(n, s, s, c, generator=g) * 3
     y[..., : c // 3] = y[..., : c // 3] * 60 + 150
     y = F.pad(y, (0, cp - c)).half()
-    gout = F.pad(torch.randn(n, so, so, c, generator=g) * gscale, (0, cp - c)).bfloat16()
+    tdt = torch.float16 if gdt == "f16" else torch.bfloat16
+    gout = F.pad(torch.randn(n, so, so, c, generator=g) * gscale, (0, cp - c)).to(tdt)
     os_ = torch.rand(n, cp, generator=g) + 0.5
     bias = torch.randn(cp, generator=g)
     yd, gd_, osd, bd = y.to(cuda), gout.to(cuda), os_.to(cuda), bias.to(cuda)
-    dc = torch.empty(n, s, s, cp, device=cuda, dtype=torch.bfloat16)
+    dc = torch.empty(n, s, s, cp, device=cuda, dtype=tdt)
     nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, cp, s, s, L.up_factor))
     ydot = torch.full([nyd], float("nan"), device=cuda)
     fu, fdn = L._fu, L._fd
     clamp = float(L.conv_clamp)
     rc = nv.load().ic2_flrelu_bwd_nhwc_ex(
-        nv.ptr(yd), nv.F16, nv.ptr(gd_), nv.BF16, nv.ptr(dc), nv.BF16, n, cp, s, s, so, so,
+        nv.ptr(yd), nv.F16, nv.ptr(gd_), nv.dtype_code(tdt), nv.ptr(dc), nv.dtype_code(tdt), n, cp, s, s, so, so,
         fu.ctypes.data_as(ctypes.c_void_p), fu.shape[0], fdn.ctypes.data_as(ctypes.c_void_p), fdn.shape[0],
         L.up_factor, L.down_factor, *L.padding, float(L.act_gain), 0.2, clamp, 0, nv.ptr(osd), nv.ptr(bd),
         nv.ptr(ydot), nyd, nv.stream_of(yd))
@@ -494,13 +555,14 @@ def test_flrelu_backward_mfma_kernel(cuda, gen256_frozen, li, gscale):
     yd_ref = (ref * (y.double()[..., :c] - bias.double()[:c])).sum(dim=(1, 2))
     yd_got = ydot.view(n, -1, cp).sum(1).cpu()[:, :c]
     ey = _rel(yd_got, yd_ref)
-    print(f"[flrelu-bwd-mfma L{li} gscale {gscale:g}] rel err gx {e:.2e}, ydot {ey:.2e}")
-    assert e < 1.2e-2
-    assert ey < 2e-2
+    print(f"[flrelu-bwd-mfma L{li} {gdt} gscale {gscale:g}] rel err gx {e:.2e}, ydot {ey:.2e}")
+    # bf16 gradient operands: 2^-9 per pass; f16 (the loss-scaled f16 training path): 2^-12
+    assert e < (1.2e-2 if gdt == "bf16" else 3e-3)
+    assert ey < (2e-2 if gdt == "bf16" else 5e-3)
 
 
 @pytest.mark.parametrize("cp,hw,n", [(512, 38 * 38, 2), (192, 278 * 277, 1), (64, 1000, 3)])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_scale_backward_kernel(cuda, cp, hw, n, dtype):
     """ic2_scale_bwd_nhwc: dx = da * xscale and d xscale = sum_p da * x (per-chunk partials summed on the host)."""
     g = torch.Generator().manual_seed(cp)
@@ -522,7 +584,7 @@ def test_scale_backward_kernel(cuda, cp, hw, n, dtype):
 
 
 @pytest.mark.parametrize("cp,hw,n", [(512, 38 * 38, 2), (192, 278 * 277, 1), (96, 1000, 3)])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_scale_forward_kernel(cuda, cp, hw, n, dtype):
     """ic2_scale_nhwc (the training path's a = x * xscale[n][c]): f32 exact, bf16 the product of the f32 scale and the
     bf16 input rounded once."""
