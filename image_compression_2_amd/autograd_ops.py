@@ -182,6 +182,35 @@ class ToNHWC(torch.autograd.Function):
         return dx, None, None
 
 
+class ScaleNHWC(torch.autograd.Function):
+    """a = x * xscale[n][c] on NHWC (ic2_scale_nhwc), differentiable in x and xscale (ic2_scale_bwd_nhwc: the per-pixel
+    sums of d xscale reduce in f32 per chunk, so an f16 activation with a loss-scaled gradient does not overflow the
+    way an f16 torch reduction over 256^2 pixels does)."""
+
+    @staticmethod
+    def forward(ctx, x, xs):
+        x = x.contiguous()
+        n, h, w, c_p = x.shape
+        xs32 = xs.detach().float().contiguous()
+        a = torch.empty_like(x)
+        nv.call("ic2_scale_nhwc", nv.ptr(x), nv.ptr(xs32), nv.ptr(a), nv.dtype_code(x.dtype), n, h * w, c_p,
+                nv.stream_of(x))
+        ctx.save_for_backward(x, xs32)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        x, xs = ctx.saved_tensors
+        n, h, w, c_p = x.shape
+        da = da.to(x.dtype).contiguous()
+        npart = int(nv.query("ic2_scale_bwd_part_floats", n, h * w, c_p))
+        part = torch.empty([npart], dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        nv.call("ic2_scale_bwd_nhwc", nv.ptr(da), nv.ptr(x), nv.ptr(xs), nv.ptr(dx), nv.dtype_code(x.dtype), n, h * w,
+                c_p, nv.ptr(part), npart, nv.stream_of(x))
+        return dx, part.view(n, -1, c_p).sum(1)
+
+
 class FrozenConvNHWC(torch.autograd.Function):
     """Conv with constant, pre-packed weights (the modulated conv of a frozen SG3 layer, whose per-sample
     modulation is applied outside as xscale / oscale): output f32, gradient w.r.t. the input only.

@@ -107,6 +107,19 @@ __device__ __forceinline__ float fb_dact(float u, float ga, float slope, float g
 #ifndef FBM_OS_DMA
 #define FBM_OS_DMA 0
 #endif
+#if FBM_OS_DMA == 2
+// diagnostic (FBM_OS_DMA=2): the DMA'd row is checked against a plain load of the same row; mismatches are counted
+// per (first item / later item), per wave, and the first one is described (item, wave, lane, got, want, and whether the
+// value read is the previous item's row)
+__device__ unsigned int g_fbm_dbg[64];
+extern "C" int ic2_fbm_debug_fetch(unsigned int* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fbm_dbg), sizeof(g_fbm_dbg), 0, hipMemcpyDeviceToHost);
+}
+extern "C" int ic2_fbm_debug_reset() {
+  unsigned int z[64] = {};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fbm_dbg), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 template <int U, int TJX, bool GF16>
 __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, int nitems, int nseg, int seg_len) {
@@ -260,11 +273,17 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
   __syncthreads();  // every wave's tap reads are done before the first GAv store overwrites the table
 
   bool first = true;
+#if FBM_OS_DMA == 2
+  int prev_w = -1;
+#endif
   for (int w = slot; w < nitems; w += gridDim.x) {
     int n, jx0, c0, t0, nt;
     item_geom(w, n, jx0, c0, t0, nt);
     const Org o = origin(jx0, t0);
     const bool has_next = w + (int)gridDim.x < nitems;
+#if FBM_OS_DMA == 2
+    const bool first_item = first;
+#endif
     if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");  // the previous item's last stores stay in flight
     first = false;
@@ -275,6 +294,32 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
     if (a.oscale) {
       if (FBM_OS_DMA) {
         osv = *reinterpret_cast<const float4*>(os_lds + 4 * g);  // landed: the wait + barrier above
+#if FBM_OS_DMA == 2
+        const float4 ref = *reinterpret_cast<const float4*>(a.oscale + (int64_t)n * a.c_p + c0 + 4 * g);
+        const float* rp = &ref.x;
+        const float* gp = &osv.x;
+        bool bad = false;
+        for (int j = 0; j < 4; ++j) bad |= __float_as_uint(rp[j]) != __float_as_uint(gp[j]);
+        if (bad) {
+          atomicAdd(&g_fbm_dbg[0], 1u);
+          atomicAdd(&g_fbm_dbg[first_item ? 1 : 2], 1u);
+          atomicAdd(&g_fbm_dbg[8 + wave], 1u);
+          atomicAdd(&g_fbm_dbg[16 + g], 1u);
+          if (prev_w >= 0) {  // is it the previous item's row?
+            int pn, pj, pc, pt, pnt;
+            item_geom(prev_w, pn, pj, pc, pt, pnt);
+            const float4 pv = *reinterpret_cast<const float4*>(a.oscale + (int64_t)pn * a.c_p + pc + 4 * g);
+            if (__float_as_uint(pv.x) == __float_as_uint(osv.x)) atomicAdd(&g_fbm_dbg[3], 1u);
+          }
+          if (atomicCAS(&g_fbm_dbg[32], 0u, 1u) == 0u) {
+            g_fbm_dbg[33] = (unsigned)w; g_fbm_dbg[34] = (unsigned)wave; g_fbm_dbg[35] = (unsigned)lane;
+            g_fbm_dbg[36] = __float_as_uint(osv.x); g_fbm_dbg[37] = __float_as_uint(ref.x);
+            g_fbm_dbg[38] = (unsigned)prev_w; g_fbm_dbg[39] = (unsigned)blockIdx.x;
+            g_fbm_dbg[40] = (unsigned)nitems; g_fbm_dbg[41] = (unsigned)gridDim.x;
+          }
+        }
+        atomicAdd(&g_fbm_dbg[4], 1u);  // rows read
+#endif
       } else {
         osv = *reinterpret_cast<const float4*>(a.oscale + (int64_t)n * a.c_p + c0 + 4 * g);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -427,6 +472,9 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
         if (U * t1 + 3 <= kend) block(U * t1 + 3, t1, std::integral_constant<int, 3>{});
       }
     }
+#if FBM_OS_DMA == 2
+    prev_w = w;
+#endif
   }
 }
 

@@ -467,8 +467,9 @@ class SynthesisLayer(torch.nn.Module):
         xs, os_ = self.modulation_train(w)
         if not self.is_torgb:
             return ao.SynthLayerNHWC.apply(x.contiguous(), xs.contiguous(), os_.contiguous(), self, dt)
-        # ToRGB (1x1, 3 channels, linear + clamp): frozen conv on MFMA, the rest as torch ops
-        a = x * xs[:, None, None, :].to(x.dtype)
+        # ToRGB (1x1, 3 channels, linear + clamp): input modulation and frozen conv as HIP kernels (the d xscale
+        # reduction in f32), the rest as torch ops
+        a = ao.ScaleNHWC.apply(x, xs)
         wp, _, bp = self.packed(dt)
         c = ao.FrozenConvNHWC.apply(a, wp, self.packed_adjoint(dt), 1, 0, self.out_channels, self.in_channels)
         y = c * os_[:, None, None, :] + bp

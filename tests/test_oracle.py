@@ -217,3 +217,16 @@ def test_parity_means_fixture(golden_dir):
         _, m, _ = oe.encoder_forward(sd, x, fine_fc1=pm.fine_fc1())
     err = (m - torch.from_numpy(fx["c2_means"][:2])).abs().max().item()
     assert err < 1e-5, err   # the same fp32 CPU computation (batch-size-dependent reduction order aside)
+
+
+def test_synthesis_grad_fixture_inputs(golden_dir):
+    """tests/golden/synthesis_grad.npz holds the oracle gradient for exactly the inputs its generator names (the GPU
+    test compares against it); its generator's frozen G matches the GPU test's fixture construction."""
+    from conftest import golden_script
+    sg = golden_script("make_synthesis_grad")
+    fx = np.load(os.path.join(golden_dir, "synthesis_grad.npz"))
+    ws, r = sg.inputs()
+    assert np.array_equal(fx["ws"], ws.numpy()) and fx["dws"].shape == (2, 16, 512)
+    assert np.isfinite(fx["dws"]).all() and np.abs(fx["dws"]).max() > 0
+    G = sg.frozen_generator()
+    assert np.allclose([float(L.magnitude_ema) for L in G.synthesis.layers()], [0.6 + 0.05 * i for i in range(15)])
