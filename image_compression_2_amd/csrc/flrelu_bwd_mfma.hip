@@ -111,12 +111,17 @@ __device__ __forceinline__ float fb_dact(float u, float ga, float slope, float g
 // diagnostic (FBM_OS_DMA=2): the DMA'd row is checked against a plain load of the same row; mismatches are counted
 // per (first item / later item), per wave, and the first one is described (item, wave, lane, got, want, and whether the
 // value read is the previous item's row)
+// g_fbm_dbg[63] is the mode: bit 0 = at the DMA's issue (block kend of the previous item) wave NW-1 waits for it and
+// checks the slot itself ([5] good, [6] bad there); [42..57] the slot's 16 dwords at the first bad read, [58..61] the
+// first LDS dword indices (of this workgroup's allocation) holding the expected value's bits, [62] the item the slot's
+// last DMA was issued for (recorded in LDS by the issuing lane)
 __device__ unsigned int g_fbm_dbg[64];
 extern "C" int ic2_fbm_debug_fetch(unsigned int* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fbm_dbg), sizeof(g_fbm_dbg), 0, hipMemcpyDeviceToHost);
 }
-extern "C" int ic2_fbm_debug_reset() {
+extern "C" int ic2_fbm_debug_reset(unsigned int mode) {
   unsigned int z[64] = {};
+  z[63] = mode;
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fbm_dbg), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 #endif
@@ -126,7 +131,7 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
   using G = FbmGeom<U, TJX>;
   constexpr int NW = G::NW, NT = 64 * NW, NBT = G::NBT, NBX = G::NBX, NINX = G::NINX, NOX = G::NOX, S = G::S;
   constexpr int OCW = G::OCW, NGX = G::NGX;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW + (FBM_OS_DMA ? 16 : 0)];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[G::LDS_DW + (FBM_OS_DMA ? (FBM_OS_DMA == 2 ? 32 : 16) : 0)];
   uint32_t* const xring = lds;
   uint32_t* const os_lds = lds + G::LDS_DW;  // FBM_OS_DMA: the item's oscale row (its own slot)
   uint32_t* const gring = lds + G::XR_DW;
@@ -232,6 +237,15 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
       const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(a.oscale + (int64_t)n * a.c_p + c0), 0, 64, 0x00020000);
       fm_dma16(prs, lane * 16, os_lds);
+#if FBM_OS_DMA == 2
+      if (lane == 0) os_lds[16] = (uint32_t)w;
+      if (g_fbm_dbg[63] & 1u) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const float want = a.oscale[(int64_t)n * a.c_p + c0 + 4 * lane];
+        const uint32_t got = os_lds[4 * lane];
+        atomicAdd(&g_fbm_dbg[got == __float_as_uint(want) ? 5 : 6], 1u);
+      }
+#endif
     }
   };
   if (slot < nitems) load_item(slot);
@@ -316,6 +330,11 @@ __global__ void __launch_bounds__(512, 4) flrelu_bwd_mfma_kernel(FlrBwdMArgs a, 
             g_fbm_dbg[36] = __float_as_uint(osv.x); g_fbm_dbg[37] = __float_as_uint(ref.x);
             g_fbm_dbg[38] = (unsigned)prev_w; g_fbm_dbg[39] = (unsigned)blockIdx.x;
             g_fbm_dbg[40] = (unsigned)nitems; g_fbm_dbg[41] = (unsigned)gridDim.x;
+            for (int j = 0; j < 16; ++j) g_fbm_dbg[42 + j] = os_lds[j];
+            int hits = 0;
+            for (int j = 0; j < G::LDS_DW + 16 && hits < 4; ++j)
+              if (lds[j] == __float_as_uint(ref.x)) g_fbm_dbg[58 + hits++] = (unsigned)j;
+            g_fbm_dbg[62] = os_lds[16];
           }
         }
         atomicAdd(&g_fbm_dbg[4], 1u);  // rows read

@@ -28,10 +28,15 @@ __device__ __forceinline__ fm_s4 fm_tr_read(const uint32_t* p) {
 // asm: the compiler then does not know an LDS write is in flight and inserts no vmcnt(0) in front of the next LDS
 // read of an unrelated buffer (which it does for the builtin, turning a prefetch into a synchronous load).  The
 // caller waits for it with an explicit s_waitcnt vmcnt before a barrier.
+// The statement opens with the wait states the hardware needs before the DMA reads its SGPR operands, which the
+// compiler pads for a builtin but cannot see inside asm: 5 after a VALU write of a descriptor SGPR (v_readlane /
+// v_readfirstlane: the compiler restores spilled descriptors with v_readlane right before the statement) and 1 after
+// the SALU write of M0.  Without them the DMA can take a stale descriptor -- zeros (out of range) or a fault -- the
+// cause of the round-3 oscale-row failures (DESIGN.md "LDS-DMA wait states").
 __device__ __forceinline__ void fm_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, const uint32_t* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)lds_dst);
-  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(m0) : "memory");
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(m0) : "memory");
 }
 
 // f32 -> f16 pairs (v_cvt_pk_f16_f32, round to nearest even)

@@ -79,6 +79,22 @@ def test_round2_entry_points_validate_before_launch():
                     1e-5, f, 1 << 20, None, 0, -1, None) == 1
 
 
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+@pytest.mark.parametrize("os_dma", [0, 1])
+def test_lds_dma_wait_states(os_dma):
+    """Every asm LDS-DMA of the strip kernels (fm_dma16) has the wait states the hardware needs in front of it: 5 after
+    a VALU write of a descriptor SGPR, 1 after the SALU write of M0 (round-3 oscale-row failures: a spilled descriptor
+    restored by v_readlane one instruction before the DMA).  Audited on the gfx950 assembly by tools/audit_lds_dma.py,
+    for the production build and the backward's oscale-row DMA (FBM_OS_DMA)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "audit_lds_dma.py"), f"-DFBM_OS_DMA={os_dma}"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 short of wait states" in r.stdout
+
+
 def test_conv_gn_rejects_f16_operands():
     """the fused conv + GroupNorm statistics path is bf16 halo-conv code.  f16 operands are
     refused at the entry point (never reach the bf16 MFMA) and the fusion query never reports f16 as fusable."""
