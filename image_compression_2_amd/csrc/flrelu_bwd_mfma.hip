@@ -101,11 +101,12 @@ __device__ __forceinline__ float fb_dact(float u, float ga, float slope, float g
   return l < lim ? ga * gs : 0.f;
 }
 
-// diagnostic build switch: 1 = the item's oscale row DMA'd into a 64-B LDS slot by four lanes of the
-// last wave with the ring groups, exactly as the forward strip kernel DMAs its post-scale row (flrelu_mfma.hip
-// flrelu_mfma3_kernel ps_lds), retired by the item-top vmcnt + barrier; 0 (default) = a plain global load per lane
+// the item's oscale row: 1 (default) = DMA'd into a 64-B LDS slot by four lanes of the last wave with the ring groups,
+// as the forward strip kernel DMAs its post-scale row (flrelu_mfma.hip flrelu_mfma3_kernel ps_lds), retired by the
+// item-top vmcnt + barrier; 0 = a plain global load per lane and a vmcnt(0) at the item top.  (Round 3 fell back to 0
+// after wrong rows; the cause was fm_dma16's missing wait states, flrelu_mfma.h; 2 = the diagnostic build that found it)
 #ifndef FBM_OS_DMA
-#define FBM_OS_DMA 0
+#define FBM_OS_DMA 1
 #endif
 #if FBM_OS_DMA == 2
 // diagnostic (FBM_OS_DMA=2): the DMA'd row is checked against a plain load of the same row; mismatches are counted
