@@ -1235,9 +1235,10 @@ int flrelu_mfma_launch(FlrArgs a, int in_f16, int up, int down, int tu, int td, 
   if ((int64_t)a.out_h * a.out_w * a.c_p * 2 >= (int64_t)FM_OOB) return IC2_E_UNSUPPORTED;  // output offsets too
   // the wide (16 x 32) tile for the f16-input synthesis path unless knob IC2_FLR_WIDE=0
   static const bool wide = knob("IC2_FLR_WIDE", 1) != 0;
-  // (only where 32-column tiles pad the output no wider than 16-column ones: not the 36-wide SG3 layers, unless
-  // knob IC2_FLR_WIDE_ALL=1)
-  static const bool wide_all = knob("IC2_FLR_WIDE_ALL", 0) != 0;
+  // everywhere, including the 36-wide SG3 layers whose 32-column strips pad the output to 64 columns (r4: 70-74 us
+  // against the 16-column tile kernel's 77 us per C2 layer, profiles/r4j_flr_wide_all.txt); knob IC2_FLR_WIDE_ALL=0
+  // keeps the tile kernel where 32-column strips would pad wider than 16-column tiles
+  static const bool wide_all = knob("IC2_FLR_WIDE_ALL", 1) != 0;
   if (in_f16 && wide && (wide_all || ceil_div(a.out_w, 32) * 32 <= ceil_div(a.out_w, 16) * 16) &&
       (int64_t)n * ceil_div(a.out_h, 16) * ceil_div(a.out_w, 32) * (a.c_p / 16) < (1LL << 31)) {
     if (up == 2) {

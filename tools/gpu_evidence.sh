@@ -1,0 +1,37 @@
+#!/bin/bash
+# Bench evidence for a round: C2 (default precision) and C4/C5 bench lines, rocprofv3 kernel traces (+ --stats) of C2
+# and C4 split into timed steps by tools/trace_steps.py, and the PMC HBM traffic of the C2 conv family
+# (tools/pmc_traffic.sh).  Each GPU step has its own time limit; the script stops at the first failure.
+#   bash tools/gpu_evidence.sh <tag> [c2 c4 c5 trace pmc]     (default: all)
+set -o pipefail
+cd $GRAFT_REPO_ROOT || exit 1
+tag=${1:-r4}; shift
+parts=${*:-"c2 c4 c5 trace pmc"}
+o=gpurun_out/$tag
+mkdir -p $o
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+run() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 300 python bench.py "$@" --out $o/${tag}_$n.json > $o/${tag}_$n.log 2>&1 || { tail -20 $o/${tag}_$n.log; exit 1; }
+  python3 -c "import json; d=json.load(open('$o/${tag}_$n.json')); r=d.get('roofline',{}); print('$n', d['value'], d['ms_per_step'], r.get('frac'), r.get('path_frac'), r.get('flr',{}).get('ms_per_step'), d.get('cpu_baseline',{}).get('value'))"
+}
+for p in $parts; do
+  case $p in
+    c2) run c2 --steps 50 --warmup 10 ;;
+    c4) run c4 --config c4 --steps 20 --warmup 5 ;;
+    c5) run c5 --config c5 --steps 20 --warmup 5 --cpu-baseline-images 0 ;;
+    trace)
+      for cfg in c2 c4; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $o/prof_$cfg -o run -- python3 bench.py --config $cfg \
+          --steps 20 --warmup 3 --cpu-baseline-images 0 --no-roofline --no-parity > $o/${tag}_prof_$cfg.log 2>&1 \
+          || { tail -20 $o/${tag}_prof_$cfg.log; exit 1; }
+        tr=$(find $o/prof_$cfg -name "*kernel_trace.csv" | head -1)
+        find $o/prof_$cfg -name "*kernel_stats.csv" -exec cp {} $o/${tag}_${cfg}_kernel_stats.csv \;
+        python3 tools/trace_steps.py $tr --warmup 3 --out $o/${tag}_${cfg}_trace_steps.txt > /dev/null || exit 1
+        gzip -c $tr > $o/${tag}_${cfg}_kernel_trace.csv.gz
+        tail -4 $o/${tag}_${cfg}_trace_steps.txt
+      done ;;
+    pmc) bash tools/pmc_traffic.sh ${tag}_pmc_traffic_c2_f16_b32 || exit 1 ;;
+  esac
+done
+echo "[evidence] done"

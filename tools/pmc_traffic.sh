@@ -11,7 +11,7 @@ i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $ctr -f csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_traffic/p$i -o run \
-    -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --cpu-baseline-images 0 --no-roofline "$@" \
+    -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --cpu-baseline-images 0 --no-roofline --no-parity "$@" \
     > gpurun_out/pmc_traffic/p$i.log 2>&1 || { echo "pass $i ($ctr) failed"; tail -5 gpurun_out/pmc_traffic/p$i.log; exit 1; }
 done
 python3 tools/pmc_traffic.py 'gpurun_out/pmc_traffic/p*' gpurun_out/pmc_traffic/$name.json "$@"
