@@ -787,7 +787,8 @@ struct FmGeom3 {
 };
 
 // diagnostic builds only (tools/build_abl.sh, wrong results): IC2_FM3_ABL bit 0 skips the ring waits, bit 1 the ring
-// DMAs, bit 2 the horizontal pass, bit 3 the vertical up, bit 4 the vertical down, bit 5 the two in-block barriers
+// DMAs, bit 2 the horizontal pass, bit 3 the vertical up, bit 4 the vertical down, bit 5 the two in-block barriers,
+// bit 6 the output stores (issued to the dropped offset: same instructions, no bytes)
 #ifndef IC2_FM3_ABL
 #define IC2_FM3_ABL 0
 #endif
@@ -1114,7 +1115,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
         const uint32_t off =
             (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
         const uint2 v = fm_out4(a.out_f16, acc_a[i][0] * ps[0], acc_a[i][1] * ps[1], acc_a[i][2] * ps[2], acc_a[i][3] * ps[3]);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, (IC2_FM3_ABL & 64) ? FM_OOB : off, 0, 0);
       }
     }
   }
