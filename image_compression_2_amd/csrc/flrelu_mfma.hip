@@ -796,6 +796,10 @@ struct FmGeom3 {
 #ifndef FM3_EARLY
 #define FM3_EARLY 1
 #endif
+// a finished tile's stores deferred into the next block, behind its ring DMA (1), or at the end of the block (0)
+#ifndef FM3_DEFER_ST
+#define FM3_DEFER_ST 1
+#endif
 template <int U, int DELTA, int NW, bool CL>
 __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs a, int nitems, int nseg, int seg_len) {
   constexpr int TOX = 32, NT = 64 * NW, RR = 16 / NW, OCW = TOX / NW;
@@ -965,9 +969,25 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
     const int kend = 2 * nt;  // blocks 0 .. kend
 
     fm_f4 acc_a[OCW], acc_b[OCW];
+    // store tile t0 + tt from acc_a: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox); exactly
+    // OCW buffer stores per wave (out-of-range pixels at the dropped offset FM_OOB)
+    auto store_tile = [&](int tt) __attribute__((always_inline)) {
+      const int gy = 16 * (t0 + tt) + li;
+#pragma unroll
+      for (int i = 0; i < OCW; ++i) {
+        const int gx = ox0 + wave + NW * i;
+        const uint32_t off =
+            (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
+        const uint2 v = fm_out4(a.out_f16, acc_a[i][0] * ps[0], acc_a[i][1] * ps[1], acc_a[i][2] * ps[2], acc_a[i][3] * ps[3]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, (IC2_FM3_ABL & 64) ? FM_OOB : off, 0, 0);
+      }
+    };
     // grid block k of the item: vertical up (ring -> V), horizontal up / activation / down (V -> D), vertical down
     // (D -> acc).  MODE 0: block 0, starts acc_b; 1: odd block, acc_a = acc_b + its share; 2: even block >= 2,
-    // finishes acc_a (stored by the caller) and starts acc_b for the next tile.
+    // finishes acc_a and starts acc_b for the next tile.  A tile finished at block k < kend is stored in block k+1,
+    // right after that block's ring DMA (acc_a is untouched until its vertical down): the stores are then younger
+    // than every DMA waited for in the next two blocks, so those waits do not wait for the stores to be written
+    // (vmcnt retires in issue order; FM3_DEFER_ST=0 stores at the end of block k)
     auto block = [&](int k, auto mode_c) __attribute__((always_inline)) {
       constexpr int MODE = decltype(mode_c)::value;
       if constexpr (!(IC2_FM3_ABL & 8)) {
@@ -999,6 +1019,9 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       // they land behind this block's horizontal pass and vertical down and the next block's vertical up
       const bool dma = !(IC2_FM3_ABL & 2) && k + 2 <= kend;
       if (FM3_EARLY && dma) load_group(n, iy0, sx0, c0, k + U + 1);
+      if constexpr (FM3_DEFER_ST && MODE == 1) {
+        if (k >= 3) store_tile((k - 3) >> 1);  // the tile block k-1 finished
+      }
 #pragma unroll
       for (int rr = 0; rr < ((IC2_FM3_ABL & 4) ? 0 : RR); ++rr) {
         const int row = wave + NW * rr;
@@ -1055,9 +1078,10 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
       // the ring group this block's DMA (issued at block k-1's barrier below) filled must have landed before
       // block k+1's vertical up: wait for it behind the stores of the tile finished at block k-1 (odd k >= 3)
       if (!(IC2_FM3_ABL & 1) && k >= 1 && k < kend) {
-        // block k-1's ring DMA must have landed (block k+1 reads it); younger: the stores of a tile finished at block
-        // k-1 (odd k >= 3: exactly OCW) and, issued early, this block's own DMA (this wave's share, uniform)
-        const bool st = MODE == 1 && k >= 3;
+        // block k-1's ring DMA must have landed (block k+1 reads it); younger: the stores of a tile (exactly OCW) --
+        // deferred: issued in this block (odd k >= 3) or in block k-1 after its DMA (even k >= 4); else issued at the
+        // end of block k-1 (odd k >= 3) -- and, issued early, this block's own DMA (this wave's share, uniform)
+        const bool st = (MODE == 1 && k >= 3) || (FM3_DEFER_ST && MODE == 2 && k >= 4);
         const int nd = FM3_EARLY && dma ? my_dma : 0;
         if (nd == 0) {
           if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OCW) : "memory");
@@ -1106,17 +1130,7 @@ __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs 
     for (int t = 0; t < nt; ++t) {
       block(2 * t + 1, std::integral_constant<int, 1>{});
       block(2 * t + 2, std::integral_constant<int, 2>{});
-      // store tile t0 + t: lane (g, oy = li) holds channels c0 + 4g .. +3 of output pixel (oy, ox); exactly OCW
-      // buffer stores per wave (out-of-range pixels at the dropped offset FM_OOB)
-      const int gy = 16 * (t0 + t) + li;
-#pragma unroll
-      for (int i = 0; i < OCW; ++i) {
-        const int gx = ox0 + wave + NW * i;
-        const uint32_t off =
-            (gy < a.out_h && gx < a.out_w) ? (uint32_t)(((gy * a.out_w + gx) * a.c_p + 4 * g) * 2) : FM_OOB;
-        const uint2 v = fm_out4(a.out_f16, acc_a[i][0] * ps[0], acc_a[i][1] * ps[1], acc_a[i][2] * ps[2], acc_a[i][3] * ps[3]);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ors, (IC2_FM3_ABL & 64) ? FM_OOB : off, 0, 0);
-      }
+      if (!FM3_DEFER_ST || t == nt - 1) store_tile(t);  // the item's last tile: stored at once (see block)
     }
   }
 }
