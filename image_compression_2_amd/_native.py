@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 import torch
@@ -177,9 +178,11 @@ def note_flops(alg_flops):
 def knob(name, default):
     """Development knob (the native library's rule, errors.hip): the environment variable `name` is read only when
     IC2_DEV=1, so the default launch plan never depends on the process environment."""
-    if os.environ.get("IC2_DEV") != "1":
-        return default
     v = os.environ.get(name)
+    if os.environ.get("IC2_DEV") != "1":
+        if v is not None:
+            print(f"[ic2] {name}={v} ignored: development knobs need IC2_DEV=1", file=sys.stderr)
+        return default
     return default if v is None else type(default)(v)
 
 

@@ -1,6 +1,7 @@
 // Thread-local error message + ABI version for libic2ops.
 #include "common.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace ic2 {
@@ -20,8 +21,13 @@ int knob(const char* name, int dflt) {
     const char* e = getenv("IC2_DEV");
     return e && e[0] == '1';
   }();
-  if (!dev) return dflt;
   const char* e = getenv(name);
+  if (!dev) {
+    // a knob set without IC2_DEV=1 is ignored: say so once per knob (an A/B script would otherwise compare default
+    // against default)
+    if (e) fprintf(stderr, "[ic2] %s=%s ignored: development knobs need IC2_DEV=1\n", name, e);
+    return dflt;
+  }
   return e ? atoi(e) : dflt;
 }
 }  // namespace ic2
