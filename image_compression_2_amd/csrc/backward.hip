@@ -176,24 +176,29 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Weight gradient, 16-bit operands (round 4): the same GEMM over pixels with 128-pixel stages, double-buffered LDS
+// Weight gradient, 16-bit operands (round 4): the same GEMM over pixels with KP-pixel stages, double-buffered LDS
 // (one barrier per stage instead of two per 32 pixels) and the j axis flattened over (tap, input channel), so a
-// 64-wide j tile of a 32-channel input covers two taps instead of reading a zero half.  Tile 64 (o) x 64 (j), 4 waves
-// of 32 x 32; per stage and wave 4 k-steps x 4 MFMAs 16x16x32.  The next stage's rows are loaded into registers
-// (4 x 16 B per operand and thread) while the current one is computed.
-template <typename T, int W2_KP>  // W2_KP: pixels per stage (64 or 128)
+// j tile of a 32-channel input covers several taps instead of reading a zero half.  Tile BT (o) x BT (j), 4 waves of
+// BT/2 x BT/2 (BT 64: 4 MFMAs 16x16x32 per 8 transposed fragment reads per k-step; BT 128: 16 per 16, for the
+// >= 128-channel layers); the next stage's rows are loaded into registers while the current one is computed.
+template <typename T, int KP, int BT>
 __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
   static_assert(sizeof(T) == 2, "16-bit operands");
-  constexpr int W2_STAGE = W2_KP * WG_PITCH;  // elements per operand and stage
-  constexpr int NQ = W2_KP / 32;              // staged rows per thread and operand
-  __shared__ __attribute__((aligned(16))) T lds[2][2][W2_STAGE];  // [stage buffer][dy | x]
+  constexpr int PITCH = BT + 8;          // LDS row pitch (elements)
+  constexpr int STAGE = KP * PITCH;      // elements per operand and stage
+  constexpr int SEGS = BT / 8;           // 16-B segments per staged row
+  constexpr int RPP = 256 / SEGS;        // rows per staging pass
+  constexpr int NQ = KP / RPP;           // staged rows per thread and operand
+  constexpr int FI = BT / 32;            // 16-wide fragments per wave and operand
+  static_assert(KP % RPP == 0 && KP % 32 == 0, "stage geometry");
+  __shared__ __attribute__((aligned(16))) T lds[2][2][STAGE];  // [stage buffer][dy | x]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
-  const int o_tiles = (a.cout_p + WG_BO - 1) / WG_BO;
-  const int o0 = (blockIdx.x % o_tiles) * WG_BO;
-  const int j0 = (blockIdx.x / o_tiles) * WG_BJ;  // flattened j = tap * cin_p + ci
+  const int o_tiles = (a.cout_p + BT - 1) / BT;
+  const int o0 = (blockIdx.x % o_tiles) * BT;
+  const int j0 = (blockIdx.x / o_tiles) * BT;  // flattened j = tap * cin_p + ci
   const int K = a.kh * a.kw * a.cin_p;
   const int c0 = (int)((int64_t)a.chunks * blockIdx.y / gridDim.y);
   const int c1 = (int)((int64_t)a.chunks * (blockIdx.y + 1) / gridDim.y);
@@ -201,8 +206,8 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
   const T* dyg = reinterpret_cast<const T*>(a.dy);
   const T* xg = reinterpret_cast<const T*>(a.x);
   const int hwo = a.ho * a.wo;
-  // staging: thread -> 8-element segment seg of rows r0 + 32 q (q < 4); the segment's j (tap, channel) is fixed
-  const int r0 = tid >> 3, seg = tid & 7;
+  // staging: thread -> 8-element segment seg of rows r0 + RPP q (q < NQ); the segment's j (tap, channel) is fixed
+  const int r0 = tid / SEGS, seg = tid % SEGS;
   const int jseg = j0 + seg * 8;
   const bool jok = jseg < K;
   const int tap = jok ? jseg / a.cin_p : 0;
@@ -210,17 +215,17 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
   const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
   const bool ook = o0 + seg * 8 < a.cout_p;
 
-  wg_f32x4 acc[2][2];
+  wg_f32x4 acc[FI][FI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FI; ++j) acc[i][j] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 vd[NQ], vx[NQ];
   auto load_stage = [&](int ch) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int p = ch * W2_KP + r0 + 32 * q;
+      const int p = ch * KP + r0 + RPP * q;
       const bool okp = p < a.P;
       const int pp = okp ? p : 0;
       const int nn = pp / hwo;
@@ -237,8 +242,8 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
   auto store_stage = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      *reinterpret_cast<uint4*>(&lds[buf][0][(r0 + 32 * q) * WG_PITCH + seg * 8]) = vd[q];
-      *reinterpret_cast<uint4*>(&lds[buf][1][(r0 + 32 * q) * WG_PITCH + seg * 8]) = vx[q];
+      *reinterpret_cast<uint4*>(&lds[buf][0][(r0 + RPP * q) * PITCH + seg * 8]) = vd[q];
+      *reinterpret_cast<uint4*>(&lds[buf][1][(r0 + RPP * q) * PITCH + seg * 8]) = vx[q];
     }
   };
   if (c0 < c1) {
@@ -252,26 +257,26 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
     const bf16_t* sdy = reinterpret_cast<const bf16_t*>(lds[buf][0]);
     const bf16_t* sx = reinterpret_cast<const bf16_t*>(lds[buf][1]);
 #pragma unroll
-    for (int ks = 0; ks < W2_KP / 32; ++ks) {
-      wg_bf16x8 af[2], bfr[2];
+    for (int ks = 0; ks < KP / 32; ++ks) {
+      wg_bf16x8 af[FI], bfr[FI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wo_ * 32 + i * 16 + 4 * tp;
-        const wg_s4 lo = wg_tr_read(sdy + (32 * ks + 8 * g + tq) * WG_PITCH + col);
-        const wg_s4 hi = wg_tr_read(sdy + (32 * ks + 8 * g + 4 + tq) * WG_PITCH + col);
+      for (int i = 0; i < FI; ++i) {
+        const int col = wo_ * (BT / 2) + i * 16 + 4 * tp;
+        const wg_s4 lo = wg_tr_read(sdy + (32 * ks + 8 * g + tq) * PITCH + col);
+        const wg_s4 hi = wg_tr_read(sdy + (32 * ks + 8 * g + 4 + tq) * PITCH + col);
         af[i] = __builtin_bit_cast(wg_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wj_ * 32 + j * 16 + 4 * tp;
-        const wg_s4 lo = wg_tr_read(sx + (32 * ks + 8 * g + tq) * WG_PITCH + col);
-        const wg_s4 hi = wg_tr_read(sx + (32 * ks + 8 * g + 4 + tq) * WG_PITCH + col);
+      for (int j = 0; j < FI; ++j) {
+        const int col = wj_ * (BT / 2) + j * 16 + 4 * tp;
+        const wg_s4 lo = wg_tr_read(sx + (32 * ks + 8 * g + tq) * PITCH + col);
+        const wg_s4 hi = wg_tr_read(sx + (32 * ks + 8 * g + 4 + tq) * PITCH + col);
         bfr[j] = __builtin_bit_cast(wg_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < FI; ++j) {
           if constexpr (std::is_same<T, _Float16>::value)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(wg_f16x8, af[i]),
                                                                __builtin_bit_cast(wg_f16x8, bfr[j]), acc[i][j], 0, 0, 0);
@@ -286,13 +291,13 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(WgradArgs a) {
   }
   float* dst = a.part + (int64_t)blockIdx.y * a.cout_p * K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FI; ++j)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int o = o0 + wo_ * 32 + i * 16 + 4 * g + rr;
-        const int jj = j0 + wj_ * 32 + j * 16 + li;
+        const int o = o0 + wo_ * (BT / 2) + i * 16 + 4 * g + rr;
+        const int jj = j0 + wj_ * (BT / 2) + j * 16 + li;
         if (o < a.cout_p && jj < K) dst[(int64_t)o * K + jj] = acc[i][j][rr];
       }
 }
@@ -305,10 +310,11 @@ static int wgrad_splits(const WgradArgs& a) {
   return (int)(sp < 1 ? 1 : sp);
 }
 
-// wgrad2_kernel's plan: j tiles over the flattened (tap, channel) axis, kp-pixel stages, `target` workgroups with at
-// least 4 stages each
-static int wgrad2_splits(const WgradArgs& a, int kp = 64, int target = 4096) {
-  const int64_t tiles = ceil_div(a.cout_p, WG_BO) * ceil_div((int64_t)a.kh * a.kw * a.cin_p, WG_BJ);
+// wgrad2_kernel's plan: bt x bt tiles, j over the flattened (tap, channel) axis, kp-pixel stages, `target`
+// workgroups with at least 4 stages each.  The 128-wide tile where both the output and the j extent fill it.
+static int wgrad2_tile(int cout_p, int K) { return cout_p >= 128 && K >= 128 ? 128 : 64; }
+static int wgrad2_splits(const WgradArgs& a, int kp = 64, int target = 4096, int bt = 64) {
+  const int64_t tiles = ceil_div(a.cout_p, bt) * ceil_div((int64_t)a.kh * a.kw * a.cin_p, bt);
   const int64_t chunks = ceil_div(a.P, kp);
   int64_t sp = ceil_div(target, tiles);
   if (sp > chunks / 4) sp = chunks / 4;
@@ -736,7 +742,7 @@ extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int 
   a.cin_p = cin_p; a.kh = kh; a.kw = kw;
   a.j_tiles = kh * kw * (int)ceil_div(cin_p, WG_BJ);
   // enough for either kernel (the 16-bit one plans its own splits)
-  const int sp = std::max(wgrad_splits(a), std::max(wgrad2_splits(a, 64, 4096), wgrad2_splits(a, 128, 2048)));
+  const int sp = std::max(wgrad_splits(a), std::max(wgrad2_splits(a, 64, 4096, 64), wgrad2_splits(a, 64, 2048, 128)));
   return (int64_t)sp * cout_p * kh * kw * cin_p;
 }
 
@@ -757,24 +763,25 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
   a.P = n * a.ho * a.wo;
   a.chunks = (int)ceil_div(a.P, WG_KP);
   a.j_tiles = kh * kw * (int)ceil_div(cin_p, WG_BJ);
-  // knob IC2_WGRAD2: 1 = 64-pixel stages (default), 2 = 128-pixel stages, 0 = the round-3 kernel for 16-bit operands too
+  // knob IC2_WGRAD2: 1 = the staged kernel, 128-wide tiles where they fill (default), 2 = 64-wide tiles only, 0 = the
+  // round-3 kernel for 16-bit operands too
   static const int v2 = knob("IC2_WGRAD2", 1);
   const bool wide = v2 != 0 && dtype != IC2_F32;
-  const int kp = v2 == 2 ? 128 : 64;
-  const int splits = wide ? wgrad2_splits(a, kp, kp == 128 ? 2048 : 4096) : wgrad_splits(a);
+  const int bt = v2 == 1 ? wgrad2_tile(cout_p, kh * kw * cin_p) : 64;
+  const int splits = wide ? wgrad2_splits(a, 64, bt == 128 ? 2048 : 4096, bt) : wgrad_splits(a);
   const int64_t total = (int64_t)cout_p * kh * kw * cin_p;
   IC2_CHECK_ARG(ws_floats >= splits * total, "conv_wgrad: workspace too small (%lld < %lld floats)",
                 (long long)ws_floats, (long long)(splits * total));
   hipStream_t s = as_stream(stream);
   if (wide) {
-    a.chunks = (int)ceil_div(a.P, kp);
-    const dim3 grid((unsigned)(ceil_div(cout_p, WG_BO) * ceil_div((int64_t)kh * kw * cin_p, WG_BJ)), (unsigned)splits);
-    if (kp == 128) {
-      if (dtype == IC2_BF16) hipLaunchKernelGGL((wgrad2_kernel<bf16_t, 128>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad2_kernel<_Float16, 128>), grid, dim3(256), 0, s, a);
+    a.chunks = (int)ceil_div(a.P, 64);
+    const dim3 grid((unsigned)(ceil_div(cout_p, bt) * ceil_div((int64_t)kh * kw * cin_p, bt)), (unsigned)splits);
+    if (bt == 128) {
+      if (dtype == IC2_BF16) hipLaunchKernelGGL((wgrad2_kernel<bf16_t, 64, 128>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad2_kernel<_Float16, 64, 128>), grid, dim3(256), 0, s, a);
     } else {
-      if (dtype == IC2_BF16) hipLaunchKernelGGL((wgrad2_kernel<bf16_t, 64>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad2_kernel<_Float16, 64>), grid, dim3(256), 0, s, a);
+      if (dtype == IC2_BF16) hipLaunchKernelGGL((wgrad2_kernel<bf16_t, 64, 64>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad2_kernel<_Float16, 64, 64>), grid, dim3(256), 0, s, a);
     }
   } else {
     const dim3 grid((unsigned)(ceil_div(cout_p, WG_BO) * a.j_tiles), (unsigned)splits);

@@ -2,7 +2,7 @@
 # Bench evidence for a round: C2 (default precision) and C4/C5 bench lines, rocprofv3 kernel traces (+ --stats) of C2
 # and C4 split into timed steps by tools/trace_steps.py, and the PMC HBM traffic of the C2 conv family
 # (tools/pmc_traffic.sh).  Each GPU step has its own time limit; the script stops at the first failure.
-#   bash tools/gpu_evidence.sh <tag> [c2 c4 c5 trace pmc]     (default: all)
+#   bash tools/gpu_evidence.sh <tag> [c2 c4 c5 trace trace5 pmc]     (default: c2 c4 c5 trace pmc)
 set -o pipefail
 cd $GRAFT_REPO_ROOT || exit 1
 tag=${1:-r4}; shift
@@ -31,6 +31,12 @@ for p in $parts; do
         gzip -c $tr > $o/${tag}_${cfg}_kernel_trace.csv.gz
         tail -4 $o/${tag}_${cfg}_trace_steps.txt
       done ;;
+    trace5)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $o/prof_c5 -o run -- python3 bench.py --config c5 \
+        --steps 10 --warmup 3 --cpu-baseline-images 0 --no-roofline > $o/${tag}_prof_c5.log 2>&1 \
+        || { tail -20 $o/${tag}_prof_c5.log; exit 1; }
+      find $o/prof_c5 -name "*kernel_stats.csv" -exec cp {} $o/${tag}_c5_kernel_stats.csv \;
+      head -25 $o/${tag}_c5_kernel_stats.csv | cut -c1-160 ;;
     pmc) bash tools/pmc_traffic.sh ${tag}_pmc_traffic_c2_f16_b32 || exit 1 ;;
   esac
 done

@@ -9,6 +9,7 @@ usage: python tools/trace_steps.py <run_kernel_trace.csv> --warmup 3 [--bench be
 import argparse
 import csv
 import json
+import re
 from collections import defaultdict
 
 CONV = ("igemm", "hg4_", "hconv_", "torgb_", "from_rgb")
@@ -20,9 +21,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--bench", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--step-end", default="uint8_sse_partial_kernel",
+                    help="regex of the kernel that closes a step (C5: the fused Adam kernel)")
+    ap.add_argument("--top", type=int, default=30)
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "uint8_sse_partial_kernel" in r["Kernel_Name"]]
+    rx = re.compile(args.step_end)
+    ends = [i for i, r in enumerate(rows) if rx.search(r["Kernel_Name"])]
     steps = [(0 if k == 0 else ends[k - 1] + 1, e + 1) for k, e in enumerate(ends)]
     timed = steps[args.warmup:]
     per = defaultdict(float)
@@ -57,7 +62,7 @@ def main():
                   f"({(fr / r['frac'] - 1) * 100:+.1f} % vs the bench), {frm:.4f} from the median step "
                   f"({(frm / r['frac'] - 1) * 100:+.1f} %); FLR {(flr / r['flr']['ms_per_step'] - 1) * 100:+.1f} %"]
     lines.append("per kernel (ms/step, calls/step):")
-    for k, v in sorted(per.items(), key=lambda kv: -kv[1])[:30]:
+    for k, v in sorted(per.items(), key=lambda kv: -kv[1])[:args.top]:
         lines.append(f"  {v / n:8.3f}  {calls[k] / n:6.1f}  {k}")
     out = "\n".join(lines)
     print(out)
