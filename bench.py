@@ -218,12 +218,13 @@ def training_flops_per_image(enc, G, res):
 def algorithmic_bytes_per_image(enc, G, res, esz, enc_split=False):
     """Compulsory HBM bytes of the conv launches per image: each conv reads its input activation and writes
     its output once (padded channel strides, esz bytes each; ToRGB writes 3 f32 channels).  enc_split: the
-    split-bf16 encoder ('bf16x3') reads its conv operands as [hi | hi | lo] bf16 (6 B per channel) and writes f32
-    (4 B); from_rgb writes the split form.  Weights are per launch, not per image, and are added by the caller."""
+    split-bf16 encoder ('bf16x3') reads its conv operands as [hi | lo] bf16 (4 B per channel; the GEMM reads the hi
+    block twice, the second time from cache) and writes f32 (4 B); from_rgb writes the split form.  Weights are per
+    launch, not per image, and are added by the caller."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
-    e_in, e_out = (6, 4) if enc_split else (esz, esz)
+    e_in, e_out = (4, 4) if enc_split else (esz, esz)
     total, h = 0.0, res
-    total += h * h * (enc.from_rgb.in_channels * 4 + p32(enc.from_rgb.out_channels) * (6 if enc_split else esz))
+    total += h * h * (enc.from_rgb.in_channels * 4 + p32(enc.from_rgb.out_channels) * (4 if enc_split else esz))
     for blk in enc.blocks:
         if h <= 1:
             break

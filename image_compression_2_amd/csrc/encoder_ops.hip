@@ -14,8 +14,9 @@ static int grid_1d(int64_t total, int per = 1) {
   return (int)g;
 }
 
-// Split-bf16 activations (ic2ops.h IC2_BF16X3): logical channel stride c_p stored as 3 * c_p bf16 channels
-// [hi | hi | lo] per pixel, hi = bf16(v), lo = bf16(v - hi) (v - hi is exact in f32).
+// Split-bf16 activations (ic2ops.h IC2_BF16X3): logical channel stride c_p stored as 2 * c_p bf16 channels
+// [hi | lo] per pixel, hi = bf16(v), lo = bf16(v - hi) (v - hi is exact in f32).  (Round 3 stored [hi | hi | lo];
+// the convs now read the hi block twice through their K mapping, igemm.hip ig_xb32.)
 struct bf16x3_t {
   bf16_t v;
 };
@@ -51,10 +52,9 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_x3_kernel(const float* __res
     if (scale) v *= scale[nn * c_p + ch];
     bf16_t hi, lo;
     split_bf16(v, hi, lo);
-    bf16_t* o = y + pix * 3 * c_p + ch;
+    bf16_t* o = y + pix * 2 * c_p + ch;
     o[0] = hi;
-    o[c_p] = hi;
-    o[2 * c_p] = lo;
+    o[c_p] = lo;
   }
 }
 
@@ -238,7 +238,7 @@ __device__ __forceinline__ void st8p(T* out, int64_t pix, int c_p, int ch0, cons
 }
 template <>
 __device__ __forceinline__ void st8p<bf16x3_t>(bf16x3_t* out, int64_t pix, int c_p, int ch0, const float (&v)[8]) {
-  bf16_t* b = reinterpret_cast<bf16_t*>(out) + pix * 3 * c_p + ch0;
+  bf16_t* b = reinterpret_cast<bf16_t*>(out) + pix * 2 * c_p + ch0;
   uint32_t h[4], l[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -248,10 +248,8 @@ __device__ __forceinline__ void st8p<bf16x3_t>(bf16x3_t* out, int64_t pix, int c
     h[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
     l[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
   }
-  const uint4 hv = make_uint4(h[0], h[1], h[2], h[3]);
-  *reinterpret_cast<uint4*>(b) = hv;
-  *reinterpret_cast<uint4*>(b + c_p) = hv;
-  *reinterpret_cast<uint4*>(b + 2 * c_p) = make_uint4(l[0], l[1], l[2], l[3]);
+  *reinterpret_cast<uint4*>(b) = make_uint4(h[0], h[1], h[2], h[3]);
+  *reinterpret_cast<uint4*>(b + c_p) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
 template <typename TI, typename TO>
@@ -391,8 +389,8 @@ __global__ void __launch_bounds__(256) gap_partial_kernel(const T* __restrict__ 
   if constexpr (std::is_same<T, bf16x3_t>::value) {
     const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
     for (int p = p0; p < p1; ++p) {
-      const bf16_t* px = xb + ((int64_t)nn * hw + p) * 3 * c_p + ch;
-      s += bf2f(px[0]) + bf2f(px[2 * c_p]);
+      const bf16_t* px = xb + ((int64_t)nn * hw + p) * 2 * c_p + ch;
+      s += bf2f(px[0]) + bf2f(px[c_p]);
     }
   } else {
     for (int p = p0; p < p1; ++p) s += ld(x + ((int64_t)nn * hw + p) * c_p + ch);
@@ -564,7 +562,7 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
 // reads).  Arithmetic: bf16 operands, f32 sums (tap order), + bias, one bf16 rounding -- as the MFMA conv.
 // ------------------------------------------------------------------------------------------------
 // X3 (the encoder's split-bf16 mode, ic2_from_rgb_conv_x3): wp is the nn.Conv2d weight itself (f32 [cout][cin][3][3],
-// `cin_p` = cout there), the image is not rounded, and the f32 result is stored split ([hi | hi | lo], 3 * COUT).
+// `cin_p` = cout there), the image is not rounded, and the f32 result is stored split ([hi | lo], 2 * COUT).
 template <int COUT, bool X3 = false>
 __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const void* __restrict__ wp,
                                                        int cin_p, const float* __restrict__ bias, bf16_t* __restrict__ y,
@@ -622,7 +620,7 @@ __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__
   const int oy = oy0 + py, ox = ox0 + px;
   if (oy >= h || ox >= w) return;
   if constexpr (X3) {
-    bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * 3 * COUT;
+    bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * 2 * COUT;
 #pragma unroll
     for (int q = 0; q < COUT / 8; ++q) {
       uint32_t hw_[4], lw_[4];
@@ -635,10 +633,8 @@ __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__
         hw_[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
         lw_[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
       }
-      const uint4 hv = make_uint4(hw_[0], hw_[1], hw_[2], hw_[3]);
-      reinterpret_cast<uint4*>(yo)[q] = hv;
-      reinterpret_cast<uint4*>(yo + COUT)[q] = hv;
-      reinterpret_cast<uint4*>(yo + 2 * COUT)[q] = make_uint4(lw_[0], lw_[1], lw_[2], lw_[3]);
+      reinterpret_cast<uint4*>(yo)[q] = make_uint4(hw_[0], hw_[1], hw_[2], hw_[3]);
+      reinterpret_cast<uint4*>(yo + COUT)[q] = make_uint4(lw_[0], lw_[1], lw_[2], lw_[3]);
     }
     return;
   }

@@ -70,7 +70,12 @@ struct IgemmArgs {
   // (sample, input channel) (mean, rstd * gamma, beta, 0) f32 [n][cin_p][4]; null = the input is used as is
   const float* in_gn;
   float in_slope;
+  // input storage: x_pix = elements per input pixel (cin_p, or 2/3 of it for the split-bf16 input, stored [hi | lo]
+  // while the GEMM's K runs over [hi | hi | lo] against [hi | lo | hi] weights); x_hb32 = 32-channel blocks of the hi
+  // part (0: plain storage).  K block b of 32 channels reads stored block ig_xb32(a, b): b, or b - x_hb32 past hi
+  int x_pix, x_hb32;
 };
+__device__ __forceinline__ int ig_xb32(const IgemmArgs& a, int b) { return b >= a.x_hb32 ? b - a.x_hb32 : b; }
 
 template <bool BF16, int BO, int BP, int WGO, int WGP, int NSTAGE>
 struct IgCfg {
@@ -271,7 +276,7 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
     // rows past M get an out-of-range y so every tap reads the zero line
     x_oy[k] = ok ? oy - a.pad : -(1 << 20);
     x_ox[k] = ox - a.pad;
-    const int64_t e = ((int64_t)(nn * a.h + x_oy[k]) * a.w_ + x_ox[k]) * a.cin_p + ch * EPC;
+    const int64_t e = ((int64_t)(nn * a.h + x_oy[k]) * a.w_ + x_ox[k]) * a.x_pix + ch * EPC;
     x_base[k] = xg + (ok ? e : 0) * ESZ;
   }
 #pragma unroll
@@ -290,14 +295,14 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
   const int q1 = (int)((int64_t)a.nq * (blockIdx.y + 1) / gridDim.y);
   // chunk cursor of the next DMA (uniform): chunk index, its tap (ky, kx) and 32-channel block
   int iq = q0, icb = q0 % CB, ikx = (q0 / CB) % a.kw, iky = (q0 / CB) / a.kw;
-  const int64_t xrow = (int64_t)a.w_ * a.cin_p * ESZ;
+  const int64_t xrow = (int64_t)a.w_ * a.x_pix * ESZ;
 
 #define IC2_IG_ISSUE(buf_)                                                                                    \
   {                                                                                                          \
     char* wl_ = lds + (buf_) * C::STAGEB;                                                                    \
     char* xl_ = wl_ + C::WB;                                                                                 \
     const int64_t wq = (int64_t)iq * 32 * ESZ;                                                               \
-    const int64_t xq = iky * xrow + ((int64_t)ikx * a.cin_p + icb * 32) * ESZ;                               \
+    const int64_t xq = iky * xrow + ((int64_t)ikx * a.x_pix + ig_xb32(a, icb) * 32) * ESZ;                    \
     _Pragma("unroll") for (int k = 0; k < NIW; ++k) {                                                        \
       const void* ws = w_base[k] ? (const void*)(w_base[k] + wq) : zero_line();                              \
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ws,                     \
@@ -491,7 +496,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
       const int oy = rem / a.wo;
       const int ox = rem - oy * a.wo;
       // offset of the output pixel's own (oy, ox) position; the descriptor base carries the tap shift
-      x_off[h][k] = (uint32_t)((((nn * a.h + oy) * a.w_ + ox) * a.cin_p + ((pch ^ ((br >> 1) & 7)) << 3)) * 2);
+      x_off[h][k] = (uint32_t)((((nn * a.h + oy) * a.w_ + ox) * a.x_pix + ((pch ^ ((br >> 1) & 7)) << 3)) * 2);
       uint32_t mask = 0;
       for (int ky = 0; ky < a.kh; ++ky)
         for (int kx = 0; kx < a.kw; ++kx) {
@@ -554,7 +559,8 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 #define IC2_G8_ISSUE_B(h_, buf_, c_)                                                                          \
   {                                                                                                          \
     const int tap = (c_).ky * a.kw + (c_).kx;                                                                \
-    const int64_t sh = ((int64_t)((c_).ky - a.pad) * a.w_ + ((c_).kx - a.pad)) * a.cin_p * 2 + (c_).cb * 128;  \
+    const int64_t sh = ((int64_t)((c_).ky - a.pad) * a.w_ + ((c_).kx - a.pad)) * a.x_pix * 2 +                \
+                       ig_xb32(a, 2 * (c_).cb) * 64;                                                          \
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(xg + sh), 0,                  \
                                                                         (c_).t < t_end ? kOob : 0, kRsrcWord3); \
     _Pragma("unroll") for (int k = 0; k < NB; ++k) {                                                         \
@@ -791,7 +797,7 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
     const int iy = oy0 - a.pad + hy, ix = ox0 - a.pad + hx;
     const bool ok = g < G::NHI && hp < G::NH && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w_;
-    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.cin_p + ((pch ^ (((hp >> 2) & 1) << 1)) << 3)) * 2)
+    h_off[k] = ok ? (uint32_t)((((nn * a.h + iy) * a.w_ + ix) * a.x_pix + ((pch ^ (((hp >> 2) & 1) << 1)) << 3)) * 2)
                   : kOob;
   }
   int brow[J];
@@ -817,7 +823,7 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
   };
   auto issue_hb = [&](int cb) {  // HB: all HPW DMAs of this wave for the halo of block cb -> halo cb & 1 (or dummy)
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 64), 0, kOob, kRsrcWord3);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)ig_xb32(a, cb) * 64), 0, kOob, kRsrcWord3);
 #pragma unroll
     for (int k = 0; k < HPW; ++k) {
       char* dst = wid + 4 * k < G::NHI ? hal + (cb & 1) * G::HALO_B + (wid + 4 * k) * 1024 : hal + 2 * G::HALO_B;
@@ -826,7 +832,7 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
   };
   auto issue_h1 = [&](int cb, int k) {  // DMA k of this wave for the halo of block cb -> halo cb & 1
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)cb * 64), 0, kOob, kRsrcWord3);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(xg + (int64_t)ig_xb32(a, cb) * 64), 0, kOob, kRsrcWord3);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         rs, (__attribute__((address_space(3))) void*)(hal + (cb & 1) * G::HALO_B + (wid + 4 * k) * 1024), 16, h_off[k],
         0, 0, 0);
@@ -1595,9 +1601,13 @@ static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, i
   const int64_t M = (int64_t)n * ho * wo;
   const int64_t x_elems = (int64_t)n * h * w_ * cin_p;
   ConvChoice c;
+  // the split-bf16 input ([hi | lo] storage) runs on the kernels whose input addressing maps the tripled K onto it
+  // (implicit GEMM, 8-phase, hg4) and is planned as the bf16 GEMM over the tripled K
+  const bool x3 = dtype == IC2_BF16X3;
+  if (x3) dtype = IC2_BF16;
   c.pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, x_elems);
   c.split384 = false;
-  if (torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype)) {
+  if (!x3 && torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype)) {
     c.kind = CK_TORGB;
     c.pl.splits = 1;
     return c;
@@ -1608,7 +1618,7 @@ static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, i
   const bool hg4_ok = hg4_eligible(dtype, cin_p, cout_p, kh, kw, x_elems, n, ho, wo);
   const bool hg4_pref = hg4_over_hconv == 1 || (hg4_over_hconv < 0 && cin_p >= 96);
   if (hg4_ok && hg4_pref) c.kind = CK_HG4;
-  else if (hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) c.kind = CK_HCONV;
+  else if (!x3 && hconv_eligible(dtype, M, cin_p, cout_p, kh, kw)) c.kind = CK_HCONV;
   else if (hg4_ok) c.kind = CK_HG4;
   else c.kind = CK_IGEMM;
   if (c.kind != CK_IGEMM) {
@@ -1651,8 +1661,11 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
 // Images per launch: the buffer-descriptor kernels (8-phase, hg4) address < 2^31 bytes per operand, so a batch whose
 // input exceeds that runs in chunks of whole images (each chunk with its own launch plan) instead of falling back to
 // the generic tile (SG3-T-1024 / the 1024^2 encoder at batch 8: 1024^2 x 192 x 2 B = 403 MB per image).
+// stored elements per input pixel: the split-bf16 input (IC2_BF16X3, cin_p = the GEMM's tripled K channels) is
+// stored [hi | lo], 2/3 of them
+static int x_pix_of(int dtype, int cin_p) { return dtype == IC2_BF16X3 ? cin_p / 3 * 2 : cin_p; }
 static int conv_chunk_n(int dtype, int n, int h, int w_, int cin_p) {
-  const int64_t per_img = (int64_t)h * w_ * cin_p * (dtype == IC2_F32 ? 4 : 2);
+  const int64_t per_img = (int64_t)h * w_ * x_pix_of(dtype, cin_p) * (dtype == IC2_F32 ? 4 : 2);
   if ((int64_t)n * per_img < (int64_t)kOob || per_img >= (int64_t)kOob) return n;
   const int64_t c = ((int64_t)kOob - 1) / per_img;
   const int64_t chunks = ceil_div(n, c);
@@ -1691,7 +1704,10 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                                  float clamp, float out_mul, int out_layout, void* workspace, int64_t ws_bytes,
                                  void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
-  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16, "conv_igemm: bad dtype %d", dtype);
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16 || dtype == IC2_BF16X3,
+                "conv_igemm: bad dtype %d", dtype);
+  IC2_CHECK_ARG(dtype != IC2_BF16X3 || (cin_p % 96 == 0 && out_layout == IC2_LAYOUT_NHWC),
+                "conv_igemm: split-bf16 input needs cin_p = 3 x a multiple of 32 and NHWC output (cin_p=%d)", cin_p);
   IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
                 "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
@@ -1706,7 +1722,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                 "conv_igemm: oscale/bias/workspace must be 16-byte aligned");
   const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
   if (nc < n) {
-    const int64_t x_img = (int64_t)h * w_ * cin_p * (dtype == IC2_F32 ? 4 : 2);
+    const int64_t x_img = (int64_t)h * w_ * x_pix_of(dtype, cin_p) * (dtype == IC2_F32 ? 4 : 2);
     const int64_t y_img = out_layout == IC2_LAYOUT_NCHW ? (int64_t)cout_valid * ho * wo * 4
                                                         : (int64_t)ho * wo * cout_p * (out_dtype == IC2_F32 ? 4 : 2);
     for (int n0 = 0; n0 < n; n0 += nc) {
@@ -1731,6 +1747,9 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.out_layout = out_layout; a.out_dtype = out_dtype;
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
   a.in_gn = nullptr; a.in_slope = 0.f;
+  a.x_pix = x_pix_of(dtype, cin_p);
+  a.x_hb32 = dtype == IC2_BF16X3 ? cin_p / 96 : 0;
+  const int kdt = dtype == IC2_BF16X3 ? IC2_BF16 : dtype;  // the kernels' operand type
   static const int group = [] {
     const int g = knob("IC2_IGEMM_GROUP", 1);  // 1 = o-tiles of a p-tile side by side (measured best)
     return g >= 1 ? g : 1;
@@ -1742,6 +1761,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.o_base = 0;
   hipStream_t s = as_stream(stream);
   ConvChoice c = conv_choice(dtype, out_layout, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  dtype = kdt;
   IgPlan& pl = c.pl;
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
   switch (c.kind) {
@@ -1789,8 +1809,8 @@ static bool x3_gn_hg4(int n, int h, int w_, int cin_p, int cout_p, int cout_vali
                       H4Plan* plan) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (ho <= 0 || wo <= 0 || groups != 32 || cout_valid != cout_p || (cout_p != 64 && cout_p != 128)) return false;
-  const int nc = conv_chunk_n(IC2_BF16, n, h, w_, cin_p);
-  const ConvChoice c = conv_choice(IC2_BF16, IC2_LAYOUT_NHWC, IC2_F32, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  const int nc = conv_chunk_n(IC2_BF16X3, n, h, w_, cin_p);
+  const ConvChoice c = conv_choice(IC2_BF16X3, IC2_LAYOUT_NHWC, IC2_F32, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
   if (c.kind != CK_HG4) return false;
   const H4Plan p = h4_plan(nc, ho, wo, cout_p);
   if (!p.tw32 || p.bo != cout_p) return false;
@@ -1838,7 +1858,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
       return -2;
     }
     if (!fuse) {
-      const int rc = ic2_conv_igemm_ws(x, w, y, IC2_BF16, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
+      const int rc = ic2_conv_igemm_ws(x, w, y, IC2_BF16X3, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
                                        ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace,
                                        ws_bytes, s);
       return rc == IC2_OK ? 0 : -1;
@@ -1853,11 +1873,13 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;
     a.in_gn = nullptr; a.in_slope = 0.f;
-    const int nc = conv_chunk_n(IC2_BF16, n, h, w_, cin_p);
+    a.x_pix = x_pix_of(IC2_BF16X3, cin_p);
+    a.x_hb32 = cin_p / 96;
+    const int nc = conv_chunk_n(IC2_BF16X3, n, h, w_, cin_p);
     const int64_t ntile = ceil_div(wo, 32) * ceil_div(ho, 8);
     for (int i0 = 0; i0 < n; i0 += nc) {  // chunks of whole images (< 2^31 input bytes per launch)
       const int cnt = n - i0 < nc ? n - i0 : nc;
-      a.x = reinterpret_cast<const char*>(x) + (int64_t)i0 * h * w_ * cin_p * 2;
+      a.x = reinterpret_cast<const char*>(x) + (int64_t)i0 * h * w_ * a.x_pix * 2;
       a.y = reinterpret_cast<char*>(y) + (int64_t)i0 * ho * wo * cout_p * 4;
       a.gn_part = part + (int64_t)i0 * groups * ntile * 2;
       a.n = cnt;
@@ -1899,6 +1921,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   a.korder = 0;
   a.o_base = 0;
   a.in_gn = in_gn; a.in_slope = in_slope;
+  a.x_pix = cin_p; a.x_hb32 = 0;
   if (fuse) {
     if (cin_p == 32 && cout_p == 32) launch_hconv<32, 32, true>(a, s);
     else if (cin_p == 32) launch_hconv<32, 64, true>(a, s);

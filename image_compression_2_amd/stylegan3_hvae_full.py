@@ -35,13 +35,13 @@ def _version_key(*tensors):
 
 class _Act:
     """NHWC activation handle: tensor [n, h, w, c_p] + logical channel count.  x3: split bf16 (ic2ops.h
-    IC2_BF16X3), the tensor holds 3 * c_p bf16 channels [hi | hi | lo] per pixel."""
+    IC2_BF16X3), the tensor holds 2 * c_p bf16 channels [hi | lo] per pixel (the convs' K runs over [hi | hi | lo])."""
     __slots__ = ("t", "n", "h", "w", "c", "c_p", "x3")
 
     def __init__(self, t, c, x3=False):
         self.t = t
         self.n, self.h, self.w, cp = t.shape
-        self.c_p = cp // 3 if x3 else cp
+        self.c_p = cp // 2 if x3 else cp
         self.c = c
         self.x3 = x3
 
@@ -114,7 +114,7 @@ def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream, split=False):
         cout_p = nv.pad32(cout)
         bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
         bp[:cout] = conv.bias.detach().float()
-        y = torch.empty([n, hh, ww, 3 * cout_p], dtype=torch.bfloat16, device=x.device)
+        y = torch.empty([n, hh, ww, 2 * cout_p], dtype=torch.bfloat16, device=x.device)
         if cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1 and cout_p in (32, 64, 128):
             wf = conv.weight.detach().to(torch.float32).contiguous()
             nv.note_flops(_conv_flops(n, hh, ww, cout, cin, 3, 3))
@@ -129,7 +129,7 @@ def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream, split=False):
             nv.note_flops(_conv_flops(n, ho, wo, cout, cin, kh, kw))
             nv.conv_igemm(nv.ptr(xf.t), nv.ptr(wp), nv.ptr(yf), nv.F32, nv.F32, n, hh, ww, xf.c_p, cout_p, cout, kh, kw,
                           pad, ho, wo, None, nv.ptr(bq), 0, 0.0, 1.0, -1.0, 1.0, nv.NCHW, stream, x.device)
-            y = torch.empty([n, ho, wo, 3 * cout_p], dtype=torch.bfloat16, device=x.device)
+            y = torch.empty([n, ho, wo, 2 * cout_p], dtype=torch.bfloat16, device=x.device)
             nv.call("ic2_nchw_to_nhwc", nv.ptr(yf), nv.ptr(y), nv.BF16X3, n, cout, ho, wo, cout_p, None, stream)
         return _Act(y, cout, x3=True)
     if (dt == torch.bfloat16 and cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1
@@ -167,10 +167,11 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
                 stream)
         return _Act(y, cout), stats
     if x.x3:
-        # split bf16: one bf16 implicit GEMM over the tripled K, f32 out, GroupNorm statistics on the f32 values
+        # split bf16: one bf16 implicit GEMM over the tripled K (its input [hi | lo] read as [hi | hi | lo]), f32 out,
+        # GroupNorm statistics on the f32 values
         y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
-        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
+        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16X3, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
                       pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.t.device)
         ya = _Act(y, cout)
         nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
@@ -230,7 +231,7 @@ def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope
         nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
                 float(norm.eps), nv.ptr(stats), stream)
     oh, ow = (y.h // 2, y.w // 2) if pool else (y.h, y.w)
-    out = torch.empty([y.n, oh, ow, 3 * y.c_p if split else y.c_p], dtype=dt, device=y.t.device)
+    out = torch.empty([y.n, oh, ow, 2 * y.c_p if split else y.c_p], dtype=dt, device=y.t.device)
     nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype),
             nv.BF16X3 if split else nv.dtype_code(dt), y.n, y.h, y.w, y.c_p, y.c, groups, nv.ptr(stats),
             nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)

@@ -10,11 +10,12 @@
  *   - dtype codes: IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2 (f16 only where an entry point says so).  Activations on the synthesis path are NHWC with a
  *     channel stride padded to a multiple of 32 ("c_p"); padded channels hold zeros.
  *   - IC2_BF16X3 = 3 (split bf16, only where an entry point says so): an f32 value v stored as hi = bf16(v),
- *     lo = bf16(v - hi).  An NHWC activation of logical stride c_p is laid out as 3 * c_p bf16 channels per pixel,
- *     [hi | hi | lo]; a packed weight as [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi].  A plain bf16 ic2_conv_igemm
- *     over cin_p' = 3 * cin_p then accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi in f32: the product to ~2^-16
- *     relative (the dropped x_lo*w_lo term is ~2^-18) at three bf16 MFMAs -- the encoder's parity mode that keeps
- *     the 8-bit latent indices of the fp32 reference.
+ *     lo = bf16(v - hi).  An NHWC activation of logical stride c_p is laid out as 2 * c_p bf16 channels per pixel,
+ *     [hi | lo] (round 3: [hi | hi | lo]); a packed weight as [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi].  The
+ *     conv entry points take such an input with dtype IC2_BF16X3 and cin_p' = 3 * cin_p: the GEMM's K runs over
+ *     [hi | hi | lo] (the hi block read twice) and accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi in f32: the product
+ *     to ~2^-16 relative (the dropped x_lo*w_lo term is ~2^-18) at three bf16 MFMAs -- the encoder's parity mode that
+ *     keeps the 8-bit latent indices of the fp32 reference.
  *
  * The reference has no native code and no C ABI: each entry point names the Python
  * function of the reference (or of the un-vendored NVlabs/stylegan3 ops it calls) that it replaces.
@@ -179,7 +180,9 @@ int ic2_dev_mode(void);
  *   y = v * out_mul  -> NHWC [n][ho][wo][cout_p] (layout 0), NCHW f32 [n][cout_valid][ho][wo] (layout 1) or
  *   channel-blocked NHWC16 [n][cout_p/16][ho][wo][16] (layout 2, any out dtype).
  * Replaces the grouped conv2d of modulated_conv2d [SG3-public] and nn.Conv2d of VGGBlock
- * (stylegan3_hvae_full.py:175-176) / from_rgb (:62).  cin_p, cout_p multiples of 32. */
+ * (stylegan3_hvae_full.py:175-176) / from_rgb (:62).  cin_p, cout_p multiples of 32.  dtype IC2_BF16X3: the
+ * split-bf16 input stored [hi | lo] (2/3 * cin_p channels per pixel), cin_p = the tripled K channel count (a multiple
+ * of 96), weights from ic2_pack_weight(IC2_BF16X3), NHWC output. */
 int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
                    int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
                    const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
@@ -206,7 +209,7 @@ int ic2_synth_input_features(const float* t, const float* freqs, const float* ph
 /* ------------------------------------------------------------------ encoder (HVAE_VGG) ---- */
 
 /* NCHW f32 -> NHWC (dtype) with channel stride c_p (zero padded), optionally times scale[n][c_p]
- * (nullable; a modulated layer's input scaling); the encoder's input packing.  dtype IC2_BF16X3: 3 * c_p channels. */
+ * (nullable; a modulated layer's input scaling); the encoder's input packing.  dtype IC2_BF16X3: 2 * c_p channels. */
 /* HVAE_VGG_Encoder.from_rgb (nn.Conv2d(cin, cout, 3, padding=1), stylegan3_hvae_full.py:62,175) read straight
  * from the NCHW f32 image: x [n][cin][h][w] f32 (cin <= 4, rounded to bf16 as ic2_nchw_to_nhwc does), w packed
  * bf16 [cout_p][3][3][cin_p] (ic2_pack_weight), bias [cout_p] f32 -> y bf16 NHWC [n][h][w][cout_p], cout_p in
@@ -215,8 +218,8 @@ int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin_p, const f
                       int w_, int cout_p, void* stream);
 
 /* The same from_rgb in the encoder's split-bf16 mode: x f32 NCHW (not rounded), w the nn.Conv2d weight as is
- * (f32 [cout][cin][3][3]), bias [cout_p] f32; exact f32 FMAs (tap order) -> y IC2_BF16X3 NHWC [n][h][w][3 * cout_p]
- * ([hi | hi | lo], the input layout of the next split-bf16 conv).  cin <= 4, cout <= cout_p, cout_p in {32, 64, 128}. */
+ * (f32 [cout][cin][3][3]), bias [cout_p] f32; exact f32 FMAs (tap order) -> y IC2_BF16X3 NHWC [n][h][w][2 * cout_p]
+ * ([hi | lo], the input layout of the next split-bf16 conv).  cin <= 4, cout <= cout_p, cout_p in {32, 64, 128}. */
 int ic2_from_rgb_conv_x3(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n, int h,
                          int w_, int cout_p, void* stream);
 
@@ -236,7 +239,7 @@ int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c
 
 /* GroupNorm apply + F.leaky_relu(0.2) (+ AvgPool2d(2,2) when pool != 0), VGGBlock.forward :183-191:
  *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling).  dtype_out may be
- *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][3 * c_p]). */
+ *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][2 * c_p]). */
 int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p, int c,
                       int groups, const float* stats, const float* gamma, const float* beta, float slope,
                       int pool, void* stream);
@@ -311,8 +314,8 @@ int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_
  * ic2_group_norm_stats runs after the conv.  stats: ic2_conv3x3_gn_stats_floats() floats (statistics + partial
  * sums); conv_ws / conv_ws_bytes: the conv's split-K workspace as for ic2_conv_igemm_ws.  fuse: 1 = fused statistics
  * where the halo conv runs, 0 = always the separate pass, -1 = default (separate; env IC2_CONV_GN=1 fuses -- measured
- * at parity on MI355X).  Deterministic.  dtype IC2_BF16X3: the split-bf16 encoder -- x bf16 with
- * cin_p = the tripled channel count ([hi | hi | lo]), w from ic2_pack_weight(IC2_BF16X3), y f32 NHWC; the
+ * at parity on MI355X).  Deterministic.  dtype IC2_BF16X3: the split-bf16 encoder -- x stored
+ * [hi | lo] with cin_p = the tripled (GEMM K) channel count, w from ic2_pack_weight(IC2_BF16X3), y f32 NHWC; the
  * statistics come out of the 4-wave halo GEMM's epilogue (on the f32 values as stored) when it runs a 64- / 128-wide
  * layer with 32 groups (fuse != 0), else the separate pass. */
 int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad,

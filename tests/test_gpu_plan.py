@@ -43,7 +43,8 @@ def _geometry(name, a):
                     pad=pad)
     if name == "ic2_conv3x3_gn_fwd":
         n, h, w, cin_p, cout_p, cv, kh, kw, pad = a[4:13]
-        return dict(dt=a[3], odt=a[3], layout=nv.NHWC, n=n, h=h, w=w, cin_p=cin_p, cout_p=cout_p, cv=cv, kh=kh, kw=kw,
+        odt = nv.F32 if a[3] == nv.BF16X3 else a[3]   # the split-bf16 conv writes f32
+        return dict(dt=a[3], odt=odt, layout=nv.NHWC, n=n, h=h, w=w, cin_p=cin_p, cout_p=cout_p, cv=cv, kh=kh, kw=kw,
                     pad=pad)
     return None   # from_rgb: its own kernels, test_gpu_kernels.py / test_gpu_split.py
 
@@ -76,6 +77,32 @@ def test_default_plan_instances_listed(default_plan_instances):
     print("[plan] instances on the benched workloads:", names)
     assert "igemm8_og2" in names and any(n.startswith("hg4_") for n in names)
     assert "igemm8_og2_f16" in names and "torgb_f16" in names  # the synthesis's f16 mode
+
+
+def _run_split(g, n, cuda):
+    """A split-bf16 geometry (dtype IC2_BF16X3: input stored [hi | lo], K over [hi | hi | lo]): the conv of the [hi | lo]
+    tensor equals, bit for bit, the plain bf16 conv of the same data tripled to [hi | hi | lo] (the round-3 storage,
+    and the tripled conv agrees with the exact-fp32 conv of the same operands -> (max|diff|, max|err vs fp32|, tol)."""
+    gen = torch.Generator().manual_seed(n * 7 + g["cin_p"])
+    c = g["cin_p"] // 3
+    ho, wo = g["h"] + 2 * g["pad"] - g["kh"] + 1, g["w"] + 2 * g["pad"] - g["kw"] + 1
+    x2 = torch.randn(n, g["h"], g["w"], 2 * c, generator=gen).to(torch.bfloat16)
+    x3 = torch.cat([x2[..., :c], x2[..., :c], x2[..., c:]], -1).contiguous()
+    w = (torch.randn(g["cout_p"], g["kh"], g["kw"], g["cin_p"], generator=gen) / (g["kh"] * g["kw"] * c) ** 0.5)
+    w = w.to(torch.bfloat16).to(cuda)
+    bias = (torch.randn(g["cout_p"], generator=gen) * 0.1).to(cuda)
+    outs = []
+    for dt, x in ((nv.BF16X3, x2), (nv.BF16, x3), (nv.F32, x3.float())):
+        xd = x.to(cuda)
+        wd = w.float() if dt == nv.F32 else w
+        y = torch.empty(n, ho, wo, g["cout_p"], dtype=torch.float32, device=cuda)
+        nv.conv_igemm(nv.ptr(xd), nv.ptr(wd), nv.ptr(y), dt, nv.F32, n, g["h"], g["w"], g["cin_p"], g["cout_p"], g["cv"],
+                      g["kh"], g["kw"], g["pad"], ho, wo, None, nv.ptr(bias), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
+                      nv.stream_of(xd), cuda)
+        torch.cuda.synchronize()
+        outs.append(y[..., :g["cv"]].cpu())
+    tol = 1e-4 * (1 + outs[2].abs().max().item())
+    return (outs[0] - outs[1]).abs().max().item(), (outs[1] - outs[2]).abs().max().item(), tol
 
 
 def _run_conv(g, n, cuda, dt_in):
@@ -117,6 +144,12 @@ def test_every_default_plan_instance_matches_fp32(cuda, default_plan_instances):
         while _plan(g, n) != p and n < g["n"]:
             n += 1
         assert _plan(g, n) == p
+        if g["dt"] == nv.BF16X3:
+            d, err, tol = _run_split(g, n, cuda)
+            print(f"[plan] {p} (split-bf16 input): n={n} {g['h']}x{g['w']} {g['cin_p']}->{g['cout_p']} "
+                  f"[hi | lo] vs tripled max|diff| {d:.2e}, vs fp32 {err:.2e}")
+            assert d == 0.0 and err < tol, p
+            continue
         got, ref = _run_conv(g, n, cuda, g["dt"])
         # f32 summation-order noise, plus one rounding of the stored output (bf16: 2^-8, f16: 2^-11 relative)
         rel = {nv.F32: 1e-4, nv.F16: 2 ** -10, nv.BF16: 2 ** -7}[g["odt"]]
