@@ -1588,6 +1588,10 @@ static void launch_hconv_cfg(const IgemmArgs& a, hipStream_t s, int cin_p, int c
 // ------------------------------------------------------------------------------------------------
 // The launch plan of ic2_conv_igemm_ws, in one place: the dispatcher, the workspace query and the plan-name query
 // (tests / bench) all read it, so what is tested and timed is what runs.
+// stored elements per input pixel: the split-bf16 input (IC2_BF16X3, cin_p = the GEMM's tripled K channels) is
+// stored [hi | lo], 2/3 of them
+static int x_pix_of(int dtype, int cin_p) { return dtype == IC2_BF16X3 ? cin_p / 3 * 2 : cin_p; }
+
 enum ConvKind { CK_TORGB, CK_HG4, CK_HCONV, CK_IGEMM };
 struct ConvChoice {
   ConvKind kind;
@@ -1599,7 +1603,7 @@ static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, i
                               int cout_valid, int kh, int kw, int pad) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
-  const int64_t x_elems = (int64_t)n * h * w_ * cin_p;
+  const int64_t x_elems = (int64_t)n * h * w_ * x_pix_of(dtype, cin_p);  // stored elements (buffer-offset limits)
   ConvChoice c;
   // the split-bf16 input ([hi | lo] storage) runs on the kernels whose input addressing maps the tripled K onto it
   // (implicit GEMM, 8-phase, hg4) and is planned as the bf16 GEMM over the tripled K
@@ -1661,9 +1665,6 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
 // Images per launch: the buffer-descriptor kernels (8-phase, hg4) address < 2^31 bytes per operand, so a batch whose
 // input exceeds that runs in chunks of whole images (each chunk with its own launch plan) instead of falling back to
 // the generic tile (SG3-T-1024 / the 1024^2 encoder at batch 8: 1024^2 x 192 x 2 B = 403 MB per image).
-// stored elements per input pixel: the split-bf16 input (IC2_BF16X3, cin_p = the GEMM's tripled K channels) is
-// stored [hi | lo], 2/3 of them
-static int x_pix_of(int dtype, int cin_p) { return dtype == IC2_BF16X3 ? cin_p / 3 * 2 : cin_p; }
 static int conv_chunk_n(int dtype, int n, int h, int w_, int cin_p) {
   const int64_t per_img = (int64_t)h * w_ * x_pix_of(dtype, cin_p) * (dtype == IC2_F32 ? 4 : 2);
   if ((int64_t)n * per_img < (int64_t)kOob || per_img >= (int64_t)kOob) return n;
