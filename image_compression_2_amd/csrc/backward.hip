@@ -312,6 +312,8 @@ static int wgrad_splits(const WgradArgs& a) {
 
 // wgrad2_kernel's plan: bt x bt tiles, j over the flattened (tap, channel) axis, kp-pixel stages, `target`
 // workgroups with at least 4 stages each.  The 128-wide tile where both the output and the j extent fill it.
+// (128 only under knob IC2_WGRAD2=3: over the encoder's layers it measured 2.4 % slower than 64 everywhere,
+// profiles/r4p_wgrad_layers.txt)
 static int wgrad2_tile(int cout_p, int K) { return cout_p >= 128 && K >= 128 ? 128 : 64; }
 static int wgrad2_splits(const WgradArgs& a, int kp = 64, int target = 4096, int bt = 64) {
   const int64_t tiles = ceil_div(a.cout_p, bt) * ceil_div((int64_t)a.kh * a.kw * a.cin_p, bt);
@@ -763,11 +765,11 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
   a.P = n * a.ho * a.wo;
   a.chunks = (int)ceil_div(a.P, WG_KP);
   a.j_tiles = kh * kw * (int)ceil_div(cin_p, WG_BJ);
-  // knob IC2_WGRAD2: 1 = the staged kernel, 128-wide tiles where they fill (default), 2 = 64-wide tiles only, 0 = the
+  // knob IC2_WGRAD2: 1 = the staged kernel, 64-wide tiles (default), 3 = 128-wide tiles where they fill, 0 = the
   // round-3 kernel for 16-bit operands too
   static const int v2 = knob("IC2_WGRAD2", 1);
   const bool wide = v2 != 0 && dtype != IC2_F32;
-  const int bt = v2 == 1 ? wgrad2_tile(cout_p, kh * kw * cin_p) : 64;
+  const int bt = v2 == 3 ? wgrad2_tile(cout_p, kh * kw * cin_p) : 64;
   const int splits = wide ? wgrad2_splits(a, 64, bt == 128 ? 2048 : 4096, bt) : wgrad_splits(a);
   const int64_t total = (int64_t)cout_p * kh * kw * cin_p;
   IC2_CHECK_ARG(ws_floats >= splits * total, "conv_wgrad: workspace too small (%lld < %lld floats)",

@@ -796,9 +796,10 @@ struct FmGeom3 {
 #ifndef FM3_EARLY
 #define FM3_EARLY 1
 #endif
-// a finished tile's stores deferred into the next block, behind its ring DMA (1), or at the end of the block (0)
+// a finished tile's stores deferred into the next block, behind its ring DMA (1), or at the end of the block (0,
+// default: the deferral measured 4 % slower over the C2 layers, profiles/r4s_flr_defer_ab.txt)
 #ifndef FM3_DEFER_ST
-#define FM3_DEFER_ST 1
+#define FM3_DEFER_ST 0
 #endif
 template <int U, int DELTA, int NW, bool CL>
 __global__ void __launch_bounds__(64 * NW, 32 / NW) flrelu_mfma3_kernel(FlrArgs a, int nitems, int nseg, int seg_len) {
