@@ -230,3 +230,16 @@ def test_synthesis_grad_fixture_inputs(golden_dir):
     assert np.isfinite(fx["dws"]).all() and np.abs(fx["dws"]).max() > 0
     G = sg.frozen_generator()
     assert np.allclose([float(L.magnitude_ema) for L in G.synthesis.layers()], [0.6 + 0.05 * i for i in range(15)])
+
+
+def test_synthesis_ref_fixture_inputs(golden_dir):
+    """tests/golden/synthesis_ref.npz (the fp64 oracle image test_gpu_path.py::test_synthesis_fp32_within_1e3_of_oracle
+    compares with) was made from exactly the seeded generator the GPU test builds and the latents it draws: the state
+    dict's sha256 and ws are re-derived here (the image itself: tests/golden/make_synthesis_ref.py, ~90 s on 8 cores)."""
+    from conftest import golden_script
+    sr = golden_script("make_synthesis_ref")
+    fx = np.load(os.path.join(golden_dir, "synthesis_ref.npz"))
+    assert np.array_equal(fx["ws"], sr.inputs().numpy())
+    assert bytes(fx["state_sha256"]).hex() == sr.state_sha(sr.generator())
+    img = fx["img"]
+    assert img.shape == (2, 3, 256, 256) and np.isfinite(img).all() and 0.05 < np.abs(img).max() < 10
