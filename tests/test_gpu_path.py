@@ -271,7 +271,8 @@ def test_pickle_loader_generator_decodes_on_gpu(cuda, tmp_path):
         assert next(G2.parameters()).is_cuda and not any(p.requires_grad for p in G2.parameters())
         img = G2.synthesis(ws.to(cuda), noise_mode="const")
         err = _maxdiff(img, ref)
-        snr = 10 * np.log10((ref ** 2).sum().item() / ((img.double().cpu() - ref) ** 2).sum().item())
+        noise = ((img.double().cpu() - ref) ** 2).sum().item()
+        snr = 10 * np.log10((ref ** 2).sum().item() / noise) if noise > 0 else float("inf")
         print(f"[loader] {precision}: max|err| {err:.2e} (output scale {scale:.1f}), SNR {snr:.1f} dB")
         if precision == "fp32":
             assert err <= 1e-6 * scale
