@@ -750,6 +750,13 @@ struct H4 {
 };
 __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
 
+// diagnostic builds only (tools/build_abl.sh hg4, wrong results): IC2_HG4_ABL bit 0 skips the multi-tap loop's
+// per-step DMA waits, bit 1 its barrier, bit 2 its fragment reads after the first step, bit 3 its MFMAs, bit 4 its
+// weight DMAs after the first step
+#ifndef IC2_HG4_ABL
+#define IC2_HG4_ABL 0
+#endif
+
 // HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
 // past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
 // chain, ~60 SALU per step) and a wait count that depends only on the tap
@@ -861,18 +868,21 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
 #pragma unroll
     for (int t = 0; t < TPB * L; ++t) issue_w(t);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI) : "memory");  // halo 0 and step 0's slabs landed
+    bf16x8 af[TPB][I], bfr[TPB][J];
     for (int s = 0; s < nst; ++s) {
-      __builtin_amdgcn_s_barrier();
+      if constexpr (!(IC2_HG4_ABL & 2)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       const int t0 = TPB * s;
+      if (!(IC2_HG4_ABL & 16) || s == 0) {
 #pragma unroll
-      for (int u = 0; u < TPB; ++u) issue_w(t0 + u + TPB * L);
+        for (int u = 0; u < TPB; ++u) issue_w(t0 + u + TPB * L);
+      }
       const bool burst = burst_at(s);  // first read >= 3 steps later
       if (burst) issue_hb(t0 / 9 + 1);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 af[TPB][I], bfr[TPB][J];
 #pragma unroll
       for (int u = 0; u < TPB; ++u) {
+        if ((IC2_HG4_ABL & 4) && s > 0) break;
         const int t = t0 + u, cb = t / 9, tap = t - cb * 9;
         // the swizzle depends on the absolute halo row: the tap shift goes into the row, not the base pointer
         const int sh = (tap / 3) * G::HW + tap % 3;
@@ -892,7 +902,10 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
 #pragma unroll
             for (int i = 0; i < I; ++i)
 #pragma unroll
-              for (int j = 0; j < J; ++j) acc[i][j] = mfma32<F16>(af[u][i], bfr[u][j], acc[i][j]);
+              for (int j = 0; j < J; ++j) {
+                if constexpr (IC2_HG4_ABL & 8) asm volatile("" ::"v"(af[u][i]), "v"(bfr[u][j]));
+                else acc[i][j] = mfma32<F16>(af[u][i], bfr[u][j], acc[i][j]);
+              }
           }
         }
       }
@@ -901,8 +914,10 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
       // step s+1's slabs landed (issued at step s+1-L); a burst of the last L steps may stay in flight (issued after
       // its step's slabs; bursts are >= 3 steps apart)
       const bool recent = burst || (L > 1 && s > 0 && burst_at(s - 1));
-      if (recent) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI + HPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI) : "memory");
+      if constexpr (!(IC2_HG4_ABL & 1)) {
+        if (recent) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI + HPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * TPB * NWI) : "memory");
+      }
     }
   } else {
 #pragma unroll

@@ -1,6 +1,7 @@
-"""Kernel microbenchmarks on the SG3-T-256 layer shapes (batch 32, bf16): FLR and implicit GEMM.
+"""Kernel microbenchmarks on the SG3-T-256 layer shapes (batch 32): FLR, implicit GEMM (bf16) and the f16 hg4
+layers (L11-L13).
 
-    python tools/bench_kernels.py [flr|igemm] [variant-env-value ...]
+    python tools/bench_kernels.py [flr|igemm|hg4] [variant-env-value ...]
 
 Each variant runs in a child process (the variant env var is read once per process).
 """
@@ -42,11 +43,16 @@ def child(kind):
                         L.down_factor, *L.padding, float(np.sqrt(2)), 0.2, 256.0, 0, None, nv.stream_of(y))
             work = 0
         else:
-            x = torch.randn(n, s_in, s_in, L.cin_p, device=dev).to(torch.bfloat16)
-            wp, _, bp = L.packed(torch.bfloat16)
-            out = torch.empty(n, conv, conv, L.cout_p, device=dev, dtype=torch.bfloat16)
+            # hg4: the f16 synthesis convs the launch plan runs on hg4 (<= 256 in, <= 192 out)
+            if kind == "hg4" and not (L.cin_p <= 256 and L.cout_p <= 192):
+                continue
+            dt = torch.float16 if kind == "hg4" else torch.bfloat16
+            cdt = nv.F16 if kind == "hg4" else nv.BF16
+            x = torch.randn(n, s_in, s_in, L.cin_p, device=dev).to(dt)
+            wp, _, bp = L.packed(dt)
+            out = torch.empty(n, conv, conv, L.cout_p, device=dev, dtype=dt)
             def run():
-                nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(out), nv.BF16, nv.BF16, n, s_in, s_in,
+                nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(wp), nv.ptr(out), cdt, cdt, n, s_in, s_in,
                         L.cin_p, L.cout_p, L.out_channels, 3, 3, 2, conv, conv, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0,
                         1.0, nv.NHWC, nv.stream_of(x))
             work = 2.0 * n * conv * conv * L.out_channels * 9 * L.in_channels
@@ -83,7 +89,7 @@ def main():
         table[v] = json.loads(r.stdout.strip().splitlines()[-1])
     names = list(next(iter(table.values())).keys()) if table else []
     print(f"{kind}: us (TFLOP/s) per layer, batch 32 bf16")
-    print(f"{'layer':14s}" + "".join(f"{v[:15]:>16s}" for v in table))
+    print(f"{'layer':14s}" + "".join(f"{v[-15:]:>16s}" for v in table))
     for nm in names:
         print(f"{nm:14s}" + "".join(f"{str(table[v][nm]):>16s}" for v in table))
     print(f"{'total us':14s}" + "".join(f"{sum(x[0] for x in table[v].values()):16.1f}" for v in table))
