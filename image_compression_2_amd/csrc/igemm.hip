@@ -744,8 +744,10 @@ struct H4 {
   static constexpr int NWI = (BO / 16 + 3) / 4;                 // weight DMA instructions per wave
   static constexpr int LDS_B = NS * WS_B + 2 * HALO_B + (HB ? 1024 : 0);  // NS-slab weight ring (+ HB dummy slot)
   static_assert(BP % TW == 0 && TW % 16 == 0, "pixel tile");
-  static_assert((BO / 16) % 4 == 0, "weight slab rows split evenly over the 4 waves");
-  static_assert(HPW <= 8, "halo DMA spread over the first 8 taps");
+  // weight slab rows split over the 4 waves: evenly, or (BO = 96) waves 2-3 issue one DMA fewer, which only the
+  // one-step lookahead of the multi-tap loop (L = 1: its waits do not count weight DMAs) allows
+  static_assert((BO / 16) % 4 == 0 || BO == 96, "weight slab rows over the 4 waves");
+  static_assert(HB || HPW <= 8, "halo DMA spread over the first 8 taps");
   static_assert(LDS_B <= 80 * 1024, "two workgroups per CU");
 };
 __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
@@ -764,6 +766,7 @@ template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool 
           bool GN = false>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = H4<I, J, WGO, WGP, TW, NS, HB>;
+  static_assert((G::BO / 16) % 4 == 0 || (TPB == 2 && NS == 4), "uneven weight DMAs need the L = 1 multi-tap loop");
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
   constexpr int NWI = G::NWI, HPW = G::HPW;
   __shared__ __attribute__((aligned(16))) char lds[G::LDS_B];
@@ -825,8 +828,9 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     char* dst = wsl + (t % NS) * G::WS_B;
 #pragma unroll
     for (int k = 0; k < NWI; ++k)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wid + 4 * k) * 1024),
-                                               16, w_off[k], 0, 0, 0);
+      if ((G::BO / 16) % 4 == 0 || wid + 4 * k < G::BO / 16)  // uneven split (BO 96): wave-uniform skip
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(dst + (wid + 4 * k) * 1024), 16, w_off[k], 0, 0, 0);
   };
   auto issue_hb = [&](int cb) {  // HB: all HPW DMAs of this wave for the halo of block cb -> halo cb & 1 (or dummy)
     const __amdgpu_buffer_rsrc_t rs =
@@ -1081,6 +1085,7 @@ IC2_HG4_KERNEL(hg4_o64_w16_s4_kernel, 4, 4, 1, 4, 16, 4)   // 64 o x (16 x 16) p
 IC2_HG4_KERNEL_P(hg4_o128_w32_p2_kernel, 8, 4, 1, 4, 32, 4, 2)  // 128 o x (8 x 32) px
 IC2_HG4_KERNEL_P(hg4_o192_w32_p2_kernel, 6, 4, 2, 2, 32, 4, 2)  // 192 o x (4 x 32) px
 IC2_HG4_KERNEL_P(hg4_o64_w32_p3_kernel, 4, 4, 1, 4, 32, 6, 3)   // 64 o x (8 x 32) px
+IC2_HG4_KERNEL_P(hg4_o96_w32_p2_kernel, 6, 4, 1, 4, 32, 4, 2)   // 96 o x (8 x 32) px
 // the split-bf16 encoder's 64- / 128-wide convs with the GroupNorm statistics of their f32 output in the epilogue
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 hg4_o64_w32_p3_gn_kernel(IgemmArgs a, int tx, int ty) {
@@ -1093,8 +1098,12 @@ hg4_o128_w32_p2_gn_kernel(IgemmArgs a, int tx, int ty) {
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_P
 
-// instance: o-tile 192 when cout_p % 192 == 0, 128 when cout_p % 128 == 0, else 64 (IC2_HG4_BO=128 forces 128 where
-// it divides); pixel tile 32 or 16 wide, whichever pads the output less
+
+// instance: o-tile 96 when cout_p % 192 == 0 (two 96-wide o-tiles on 8 x 32-pixel tiles: a weight slab feeds 256
+// pixels instead of the 192-wide tile's 128, so 2.1 instead of 3.4 LDS-DMA pieces per 24 MFMAs; SG3-T-256 L11
+// 2.27 -> 2.15 ms, profiles/r4x_hg4_o96.txt), 128 when cout_p % 128 == 0, else 64; IC2_HG4_BO = 192 / 128 / 96 / 64
+// forces one where it divides.  Pixel tile 32 or 16 wide, whichever pads the output less (a 96-wide o-tile whose
+// output pads less on 16-wide tiles runs as the 192-wide 16-wide-tile instance).
 struct H4Plan {
   int bo;
   bool tw32;
@@ -1103,13 +1112,15 @@ struct H4Plan {
 static H4Plan h4_plan(int n, int ho, int wo, int cout_p) {
   static const int force_bo = knob("IC2_HG4_BO", 0);
   H4Plan p;
-  p.bo = cout_p % 192 == 0 ? 192 : cout_p % 128 == 0 ? 128 : 64;
-  if (force_bo == 128 && cout_p % 128 == 0) p.bo = 128;
-  const int bp = p.bo <= 128 ? 256 : 128;
-  const int th32 = bp / 32, th16 = bp / 16;
+  p.bo = cout_p % 192 == 0 ? 96 : cout_p % 128 == 0 ? 128 : 64;
+  if ((force_bo == 192 || force_bo == 128 || force_bo == 96 || force_bo == 64) && cout_p % force_bo == 0)
+    p.bo = force_bo;
+  const int bp32 = p.bo <= 128 ? 256 : 128, bp16 = p.bo <= 128 && p.bo != 96 ? 256 : 128;
+  const int th32 = bp32 / 32, th16 = bp16 / 16;
   const int64_t a32 = ceil_div(ho, th32) * th32 * ceil_div(wo, 32) * 32;
   const int64_t a16 = ceil_div(ho, th16) * th16 * ceil_div(wo, 16) * 16;
   p.tw32 = a32 <= a16;
+  if (p.bo == 96 && !p.tw32) p.bo = 192;
   const int64_t tiles = p.tw32 ? ceil_div(ho, th32) * ceil_div(wo, 32) : ceil_div(ho, th16) * ceil_div(wo, 16);
   p.blocks = n * tiles * ceil_div(cout_p, p.bo);
   return p;
@@ -1131,6 +1142,7 @@ static void hg4_dispatch(const IgemmArgs& a, hipStream_t s, bool f16) {
   if (p.tw32) {
     if (p.bo == 192) launch_hg4<6, 4, 2, 2, 32>(a, s, f16 ? hg4_o192_w32_p2_kernel_f16 : hg4_o192_w32_p2_kernel);
     else if (p.bo == 128) launch_hg4<8, 4, 1, 4, 32>(a, s, f16 ? hg4_o128_w32_p2_kernel_f16 : hg4_o128_w32_p2_kernel);
+    else if (p.bo == 96) launch_hg4<6, 4, 1, 4, 32>(a, s, f16 ? hg4_o96_w32_p2_kernel_f16 : hg4_o96_w32_p2_kernel);
     else launch_hg4<4, 4, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_p3_kernel_f16 : hg4_o64_w32_p3_kernel);
   } else {
     if (p.bo == 192) launch_hg4<6, 4, 2, 2, 16>(a, s, f16 ? hg4_o192_w16_s4_kernel_f16 : hg4_o192_w16_s4_kernel);

@@ -388,13 +388,28 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad, dtype):
 @pytest.mark.parametrize("dtype", ["torch.bfloat16", "torch.float16"])
 def test_conv_halo_gemm4(cuda, cin, cout, size, pad, dtype):
     """The 4-wave halo implicit GEMM (hg4: 32-channel blocks, two workgroups per CU) forced on every instance
-    (knob IC2_HG4=2 under IC2_DEV=1, read once per process, so in a child process): 64 / 128 / 192 output channels
+    (knob IC2_HG4=2 under IC2_DEV=1, read once per process, so in a child process): 64 / 96 / 128 / 192 output channels
     per workgroup, 8 x 32 / 16 x 16 / 4 x 32 / 8 x 16 pixel tiles, cin_p a multiple of 32 but not of 64 (96, 192 -> 192),
     partial o-tiles (320 = 2.5 x 128), ragged tile edges, pad 1 and 2 -- against F.conv2d in fp64."""
     import subprocess, sys
     code = (f"import sys, torch; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
             f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},{dtype},n=4)")
     env = dict(__import__('os').environ, IC2_DEV="1", IC2_HG4="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("cin,cout,size,pad", [(128, 181, 40, 2), (256, 192, 31, 2), (64, 192, 30, 1)])
+@pytest.mark.parametrize("dtype", ["torch.bfloat16", "torch.float16"])
+@pytest.mark.parametrize("bo", [96, 192])
+def test_conv_halo_gemm4_o192_outputs(cuda, cin, cout, size, pad, dtype, bo):
+    """192-wide outputs on either hg4 instance, forced with IC2_HG4_BO in a child process: two 96-wide o-tiles (the
+    default; waves 2-3 issue one weight DMA fewer per tap) or one 192-wide o-tile, against F.conv2d in fp64:
+    181 -> 192 padded outputs, ragged tiles."""
+    import subprocess, sys
+    code = (f"import sys, torch; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
+            f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},{dtype},n=4)")
+    env = dict(__import__('os').environ, IC2_DEV="1", IC2_HG4="2", IC2_HG4_BO=str(bo))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
 

@@ -232,8 +232,10 @@ def test_conv_launch_plan_names():
     assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 148, 148, 512, 512, 512, 3, 3, 2) == "igemm8_og2"
     # L9 (512 -> 362, cout_p 384): 256-wide + 128 x 512 launches
     assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 148, 148, 512, 384, 362, 3, 3, 2) == "igemm8_og2+og1"
-    # L11 (256 -> 181 at 276^2, cout_p 192): the 4-wave halo GEMM
-    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 276, 276, 256, 192, 181, 3, 3, 2).startswith("hg4_o192")
+    # L11 (256 -> 181 at 276^2, cout_p 192): the 4-wave halo GEMM, two 96-wide o-tiles on 8 x 32-pixel tiles
+    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 276, 276, 256, 192, 181, 3, 3, 2) == "hg4_o96_w32_p2"
+    # a 192-wide output that pads less on 16-wide pixel tiles keeps the 192-wide 16-wide-tile instance
+    assert plan(nv.BF16, nv.F16, nv.NHWC16, B, 47, 47, 256, 192, 192, 3, 3, 1) == "hg4_o192_w16_s4"
     # ToRGB: the VALU 1x1 kernel
     assert plan(nv.BF16, nv.F32, nv.NCHW, B, 256, 256, 128, 32, 3, 1, 1, 0) == "torgb"
     # encoder block 0 conv2 in bf16 (64 -> 64 at 256^2): the halo direct conv; split-bf16 (192 tripled channels): hg4
