@@ -96,7 +96,8 @@ class Conv2dNHWC(torch.autograd.Function):
                     cout_p, kh, kw, ctx.pad, nv.ptr(ws), nfl, nv.stream_of(x))
             dw = dwp[:cout, :, :, :cin].permute(0, 3, 1, 2).contiguous()
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.reshape(-1, cout_p)[:, :cout].float().sum(0)
+            # f32 accumulation straight from the 16-bit gradient (no f32 copy of dy)
+            db = dy.reshape(-1, cout_p).sum(0, dtype=torch.float32)[:cout]
         return dx, dw, db, None, None
 
 
