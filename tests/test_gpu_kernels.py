@@ -355,20 +355,45 @@ IGEMM_CASES = [(3, 32, 19, 1, 0), (64, 96, 12, 1, 0), (181, 128, 9, 2, 0), (512,
                (64, 362, 10, 1, 7)]
 
 
-@pytest.mark.parametrize("cin,cout,size,pad,tile", IGEMM_CASES)
+def _child_conv_cases(env, cases, dtype, n=None):
+    """_conv_case over `cases` in ONE child process with the knob environment `env` (the knobs are read once per
+    process); the child tries every case and reports all that fail."""
+    import subprocess, sys
+    code = (f"import sys, torch; sys.path.insert(0, {repr(str(os.getcwd()))});"
+            f"from tests.test_gpu_kernels import _conv_cases_report; _conv_cases_report({cases!r}, {dtype}, {n!r})")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, IC2_DEV="1", **env), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+
+
+def _conv_cases_report(cases, dtype, n=None):
+    bad = []
+    for c in cases:
+        try:
+            _conv_case(*c, dtype=dtype, **({"n": n} if n else {}))
+        except AssertionError as e:
+            bad.append((c, str(e)[:300]))
+    assert not bad, f"failing cases: {bad}"
+
+
+@pytest.mark.parametrize("cin,cout,size,pad,tile", [c for c in IGEMM_CASES if c[4] == 0])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-def test_conv_igemm(cuda, cin, cout, size, pad, tile, dtype, monkeypatch):
-    """Every bf16 / f16 tile instance (knob IC2_IGEMM_TILE under IC2_DEV=1 forces it; read once per process, so the
-    forced cases run in a child process) against F.conv2d in fp64."""
-    if tile and dtype != torch.float32:
-        import subprocess, sys
-        code = (f"import sys, torch; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
-                f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},{dtype})")
-        env = dict(__import__('os').environ, IC2_DEV="1", IC2_IGEMM_TILE=str(tile))
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stdout + r.stderr
-        return
+def test_conv_igemm(cuda, cin, cout, size, pad, tile, dtype):
+    """The default plan's implicit-GEMM instances against F.conv2d in fp64."""
     _conv_case(cin, cout, size, pad, dtype)
+
+
+@pytest.mark.parametrize("tile", sorted({c[4] for c in IGEMM_CASES} - {0}))
+@pytest.mark.parametrize("dtype", [torch.float32, "torch.bfloat16", "torch.float16"])
+def test_conv_igemm_forced_tiles(cuda, tile, dtype):
+    """Every bf16 / f16 tile instance, forced by the knob IC2_IGEMM_TILE (IC2_DEV=1; read once per process, so each
+    tile's cases run in one child process), against F.conv2d in fp64; fp32 has one tile and runs in-process."""
+    cases = [c[:4] for c in IGEMM_CASES if c[4] == tile]
+    if dtype == torch.float32:
+        for c in cases:
+            _conv_case(*c, dtype)
+        return
+    _child_conv_cases({"IC2_IGEMM_TILE": str(tile)}, cases, dtype)
 
 
 @pytest.mark.parametrize("cin,cout,size,pad", [(32, 32, 150, 1), (3, 32, 160, 1), (32, 64, 151, 2), (64, 32, 149, 2),
@@ -381,37 +406,28 @@ def test_conv_halo_kernel(cuda, cin, cout, size, pad, dtype):
     _conv_case(cin, cout, size, pad, dtype)
 
 
-@pytest.mark.parametrize("cin,cout,size,pad", [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1),
-                                              (256, 256, 30, 2), (32, 256, 29, 1), (128, 384, 20, 1), (64, 320, 21, 1),
-                                              (181, 128, 37, 2), (81, 51, 37, 2), (64, 64, 33, 1), (384, 128, 24, 1),
-                                              (512, 192, 21, 1)])
+HG4_CASES = [(64, 128, 45, 2), (96, 128, 40, 1), (128, 181, 40, 2), (192, 192, 33, 1), (256, 256, 30, 2),
+             (32, 256, 29, 1), (128, 384, 20, 1), (64, 320, 21, 1), (181, 128, 37, 2), (81, 51, 37, 2), (64, 64, 33, 1),
+             (384, 128, 24, 1), (512, 192, 21, 1)]
+
+
 @pytest.mark.parametrize("dtype", ["torch.bfloat16", "torch.float16"])
-def test_conv_halo_gemm4(cuda, cin, cout, size, pad, dtype):
+def test_conv_halo_gemm4(cuda, dtype):
     """The 4-wave halo implicit GEMM (hg4: 32-channel blocks, two workgroups per CU) forced on every instance
     (knob IC2_HG4=2 under IC2_DEV=1, read once per process, so in a child process): 64 / 96 / 128 / 192 output channels
     per workgroup, 8 x 32 / 16 x 16 / 4 x 32 / 8 x 16 pixel tiles, cin_p a multiple of 32 but not of 64 (96, 192 -> 192),
     partial o-tiles (320 = 2.5 x 128), ragged tile edges, pad 1 and 2 -- against F.conv2d in fp64."""
-    import subprocess, sys
-    code = (f"import sys, torch; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
-            f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},{dtype},n=4)")
-    env = dict(__import__('os').environ, IC2_DEV="1", IC2_HG4="2")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
+    _child_conv_cases({"IC2_HG4": "2"}, HG4_CASES, dtype, n=4)
 
 
-@pytest.mark.parametrize("cin,cout,size,pad", [(128, 181, 40, 2), (256, 192, 31, 2), (64, 192, 30, 1)])
 @pytest.mark.parametrize("dtype", ["torch.bfloat16", "torch.float16"])
 @pytest.mark.parametrize("bo", [96, 192])
-def test_conv_halo_gemm4_o192_outputs(cuda, cin, cout, size, pad, dtype, bo):
+def test_conv_halo_gemm4_o192_outputs(cuda, dtype, bo):
     """192-wide outputs on either hg4 instance, forced with IC2_HG4_BO in a child process: two 96-wide o-tiles (the
     default; waves 2-3 issue one weight DMA fewer per tap) or one 192-wide o-tile, against F.conv2d in fp64:
     181 -> 192 padded outputs, ragged tiles."""
-    import subprocess, sys
-    code = (f"import sys, torch; sys.path.insert(0, {repr(str(__import__('os').getcwd()))});"
-            f"from tests.test_gpu_kernels import _conv_case; _conv_case({cin},{cout},{size},{pad},{dtype},n=4)")
-    env = dict(__import__('os').environ, IC2_DEV="1", IC2_HG4="2", IC2_HG4_BO=str(bo))
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
+    _child_conv_cases({"IC2_HG4": "2", "IC2_HG4_BO": str(bo)}, [(128, 181, 40, 2), (256, 192, 31, 2), (64, 192, 30, 1)],
+                      dtype, n=4)
 
 
 @pytest.mark.parametrize("cin,cout,size,pad,n", [(512, 512, 12, 1, 3), (1024, 320, 9, 1, 2), (768, 256, 7, 2, 5),
