@@ -26,6 +26,7 @@ their styles only:
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -47,6 +48,33 @@ def pack_conv_weight(weight, cin_p, cout_p, dt):
     return out
 
 
+_DERIVED = None  # dict while a derived_cache() block is active
+
+
+@contextlib.contextmanager
+def derived_cache():
+    """Inside the block, data derived from a parameter (packed and adjoint conv weights, the padded bias) is built
+    once and reused: the training step runs the encoder twice on the same weights (ref :670-671), forward and
+    backward.  The parameters must not change inside the block (training.train_step steps the optimizer after it;
+    a fused optimizer does not bump version counters, so the cache is scoped, not versioned)."""
+    global _DERIVED
+    prev, _DERIVED = _DERIVED, {}
+    try:
+        yield
+    finally:
+        _DERIVED = prev
+
+
+def _derived(t, key, make):
+    if _DERIVED is None or not isinstance(t, torch.nn.Parameter):  # temporaries: ids and storage get reused
+        return make()
+    k = (id(t), t.data_ptr()) + key
+    hit = _DERIVED.get(k)
+    if hit is None:
+        hit = _DERIVED[k] = make()
+    return hit
+
+
 def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None):
     n, h, w, cin_p = x.shape
     cout_p = wp.shape[0]
@@ -66,12 +94,17 @@ class Conv2dNHWC(torch.autograd.Function):
     def forward(ctx, x, weight, bias, pad, cout_p):
         cout, cin, kh, kw = weight.shape
         cin_p = x.shape[-1]
-        wp = pack_conv_weight(weight, cin_p, cout_p, x.dtype)
-        bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
-        if bias is not None:
-            bp[:cout] = bias.detach().float()
+        wp = _derived(weight, ("fwd", cin_p, cout_p, x.dtype), lambda: pack_conv_weight(weight, cin_p, cout_p, x.dtype))
+
+        def padded_bias():
+            bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
+            if bias is not None:
+                bp[:cout] = bias.detach().float()
+            return bp
+        bp = _derived(bias if bias is not None else weight, ("bias", cout_p), padded_bias)
         y = conv_nhwc(x, wp, bp, cout, kh, pad)
         ctx.save_for_backward(x, weight)
+        ctx.weight = weight  # the parameter object itself: the key of its derived-data cache
         ctx.pad, ctx.has_bias = pad, bias is not None
         return y
 
@@ -85,8 +118,8 @@ class Conv2dNHWC(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dx = conv(dy, W flipped in space, transposed in channels), padding k - 1 - pad
-            wt = weight.detach().transpose(0, 1).flip(2, 3)
-            wtp = pack_conv_weight(wt, cout_p, cin_p, x.dtype)
+            wtp = _derived(ctx.weight, ("adj", cin_p, cout_p, x.dtype),
+                           lambda: pack_conv_weight(weight.detach().transpose(0, 1).flip(2, 3), cout_p, cin_p, x.dtype))
             dx = conv_nhwc(dy, wtp, None, cin_p, kh, kh - 1 - ctx.pad)
         if ctx.needs_input_grad[1]:
             nfl = int(nv.query("ic2_conv_wgrad_ws_floats", n, h, w, cin_p, cout_p, kh, kw, ctx.pad))

@@ -30,6 +30,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from . import autograd_ops as ao
 from . import distributed as icd
 
 
@@ -86,7 +87,7 @@ def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_
 
 def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight, percep,
                 second_encoder_pass, sync_gradients, scaler=None):
-    with torch.enable_grad():
+    with torch.enable_grad(), ao.derived_cache():
         if second_encoder_pass:
             reconstructed, _ = compressor(images)
             _, means, logvars = encoder(images)
