@@ -165,3 +165,31 @@ def test_fix_fine_projector_builds_fc1_for_the_pooled_width():
     assert enc.fine_projector.fc1.weight.shape == (256, 128) and enc.fine_projector.in_channels == 128
     assert ref.fine_projector.fc1.weight.shape == (256, 64)
     assert enc.global_projector.in_channels == 512 and enc.medium_projector.in_channels == 512
+
+
+def test_derived_cache_scope():
+    """autograd_ops.derived_cache: inside the block a parameter's derived data (packed weights, padded bias) is
+    built once per key and reused; outside it, and for non-parameter temporaries, it is rebuilt every call (a fused
+    optimizer does not bump version counters, so the cache is scoped to the training step, not versioned)."""
+    from image_compression_2_amd import autograd_ops as ao
+    p = torch.nn.Parameter(torch.randn(4))
+    calls = []
+
+    def make():
+        calls.append(1)
+        return torch.zeros(1)
+    ao._derived(p, ("k",), make)
+    ao._derived(p, ("k",), make)
+    assert len(calls) == 2                      # no block: no caching
+    with ao.derived_cache():
+        a = ao._derived(p, ("k",), make)
+        b = ao._derived(p, ("k",), make)
+        assert a is b and len(calls) == 3       # one build per key
+        ao._derived(p, ("other",), make)
+        assert len(calls) == 4
+        t = p.detach() * 2                      # a temporary: never cached
+        ao._derived(t, ("k",), make)
+        ao._derived(t, ("k",), make)
+        assert len(calls) == 6
+    ao._derived(p, ("k",), make)
+    assert len(calls) == 7                      # the block's entries are gone
