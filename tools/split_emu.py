@@ -1,6 +1,6 @@
 """CPU emulation of the encoder precision candidates against the fp32 oracle: each conv computed
 in fp64 on operands rounded / split as a mode would store them, conv outputs f32; 8-bit index flips vs the oracle.
-    python tools/split_emu.py B mode [mode ...]   (modes: fp64 bf16 f16 split_bf16 split_f16 x2_* w2_*)"""
+    python tools/split_emu.py B mode [mode ...]   (modes: fp64 bf16 f16 split_bf16 split_f16 x2_* w2_* mixK tailK)"""
 import sys, torch, torch.nn.functional as F, time
 sys.path.insert(0, '/root/repo')
 import image_compression_2_amd as ic2
@@ -25,12 +25,17 @@ CONV_IDX = [0]
 
 def make_conv(mode):
     base = mode
-    if mode.startswith('mix'):   # mixK: the first K convs (from_rgb = 0, block0 conv1 = 1, ...) in bf16, the rest split
-        k = int(mode[3:])
+    if mode.startswith('mix') or mode.startswith('tail'):
+        # mixK: the first K convs (from_rgb = 0, block i conv1 = 1 + 2i, conv2 = 2 + 2i) in bf16, the rest split;
+        # tailK: the convs from index K on in bf16, the ones before split
+        k = int(mode[3:] if mode.startswith('mix') else mode[4:])
     def conv(x, w, b):
         mode = base
         if base.startswith('mix'):
             mode = 'bf16' if CONV_IDX[0] < k else 'split_bf16'
+            CONV_IDX[0] += 1
+        elif base.startswith('tail'):
+            mode = 'bf16' if CONV_IDX[0] >= k else 'split_bf16'
             CONV_IDX[0] += 1
         if mode == 'fp64':
             y = F.conv2d(x.double(), w.double(), b.double(), padding=1)
@@ -60,6 +65,9 @@ def enc_forward(mode):
     if mode.startswith('mix'):  # activations stored bf16 while the convs consuming them are bf16
         k = int(mode[3:])
         store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] < k else t
+    if mode.startswith('tail'):
+        k = int(mode[4:])
+        store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] >= k else t
     h = store(conv(x, sd['from_rgb.weight'], sd['from_rgb.bias']))
     feats = {}
     for i in range(10):
