@@ -772,7 +772,7 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
   const int bt = v2 == 3 ? wgrad2_tile(cout_p, kh * kw * cin_p) : 64;
   // knob IC2_WGRAD_TARGET: workgroups per launch the K split aims at (64-wide tiles; the split-K partials it writes
   // are re-read by wgrad_reduce_kernel)
-  static const int target = knob("IC2_WGRAD_TARGET", 4096);
+  static const int target = std::max(64, std::min(knob("IC2_WGRAD_TARGET", 4096), 4096));  // <= the workspace plan's
   const int splits = wide ? wgrad2_splits(a, 64, bt == 128 ? target / 2 : target, bt) : wgrad_splits(a);
   const int64_t total = (int64_t)cout_p * kh * kw * cin_p;
   IC2_CHECK_ARG(ws_floats >= splits * total, "conv_wgrad: workspace too small (%lld < %lld floats)",
