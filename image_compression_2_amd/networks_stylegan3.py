@@ -187,6 +187,18 @@ class SynthesisInput(torch.nn.Module):
                       feats.device)
         return out
 
+    def _train_grid(self, device):
+        """The sampling grid of the Fourier features (constant): built once per device.  Built on every call, its
+        host-side theta was a blocking host-to-device copy that drained the stream once per training step."""
+        g = getattr(self, "_grid_cache", None)
+        if g is None or g.device != device:
+            S = int(self.size[0])
+            theta = torch.tensor([[0.5 * S / self.sampling_rate, 0, 0], [0, 0.5 * S / self.sampling_rate, 0]],
+                                 dtype=torch.float32)
+            g = F.affine_grid(theta.unsqueeze(0), [1, 1, S, S], align_corners=False).to(device)
+            self._grid_cache = g
+        return g
+
     def forward_train_nhwc(self, w, dt=torch.float32):
         """Autograd path: w [n, w_dim] -> NHWC [n, S, S, C] features (dt), as torch ops (SG3
         SynthesisInput.forward: affine -> rotation/translation of the Fourier frequencies -> sin features with
@@ -206,10 +218,7 @@ class SynthesisInput(torch.nn.Module):
         phases = self.phases.float().unsqueeze(0) + (freqs @ transforms[:, :2, 2:]).squeeze(2)
         freqs = freqs @ transforms[:, :2, :2]
         amplitudes = (1 - (freqs.norm(dim=2) - self.bandwidth) / (self.sampling_rate / 2 - self.bandwidth)).clamp(0, 1)
-        S = int(self.size[0])
-        theta = torch.tensor([[0.5 * S / self.sampling_rate, 0, 0], [0, 0.5 * S / self.sampling_rate, 0]],
-                             dtype=torch.float32, device=w.device)
-        grids = F.affine_grid(theta.unsqueeze(0), [1, 1, S, S], align_corners=False)     # [1, S, S, 2]
+        grids = self._train_grid(w.device)  # [1, S, S, 2]
         # grid . freq as two broadcast products (a K = 2 batched matmul here, and its backward over the 36 x 36 grid,
         # ran as two ~0.45 ms library GEMMs per C5 step)
         x = grids[0, :, :, 0, None] * freqs[:, None, None, :, 0] + grids[0, :, :, 1, None] * freqs[:, None, None, :, 1]
