@@ -75,6 +75,27 @@ def _derived(t, key, make):
     return hit
 
 
+class SplitRows(torch.autograd.Function):
+    """[L, n, c] -> L contiguous [n, widths[l]] leading-column slices; the backward writes every slice's gradient
+    into one zero-initialised [L, n, c] tensor (one fill and L copies, where autograd's per-slice backward would
+    build L full-size zero tensors and add them)."""
+
+    @staticmethod
+    def forward(ctx, t, widths):
+        ctx.shape = t.shape
+        return tuple(t[i, :, :w].contiguous() for i, w in enumerate(widths))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        g = None
+        for i, gi in enumerate(grads):
+            if gi is not None:
+                if g is None:
+                    g = gi.new_zeros(ctx.shape)
+                g[i, :, : gi.shape[1]].copy_(gi)
+        return g, None
+
+
 def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None):
     n, h, w, cin_p = x.shape
     cout_p = wp.shape[0]

@@ -704,12 +704,13 @@ class SynthesisNetwork(torch.nn.Module):
         st = torch.baddbmm(bst.unsqueeze(1), wl, wst.transpose(1, 2))       # styles [L, n, cm], 0 past cin
         s = st * (st.square().sum(dim=(1, 2)) / (cin * n)).rsqrt()[:, None, None]
         d = (torch.bmm(s.square(), wsq.transpose(1, 2)) + 1e-8).rsqrt() * igm  # [L, n, om], 0 past cout
+        xss = ao.SplitRows.apply(s, tuple(L.cin_p for L in convs))
+        oss = ao.SplitRows.apply(d, tuple(L.cout_p for L in convs))
         for i, L in enumerate(layers):
             if L.is_torgb:
                 x = L.forward_train_nhwc(x, ws[:, i + 1], dt, final_scale=self.output_scale)
             else:
-                x = ao.SynthLayerNHWC.apply(x.contiguous(), s[i, :, : L.cin_p].contiguous(),
-                                            d[i, :, : L.cout_p].contiguous(), L, dt)
+                x = ao.SynthLayerNHWC.apply(x.contiguous(), xss[i], oss[i], L, dt)
         return x
 
     def extra_repr(self):
