@@ -1,5 +1,6 @@
-"""Where the C5 training step's small torch launches come from: torch.profiler over two steps of the bench's C5
-setup (f16 + loss scaler), ATen ops grouped by the innermost package frames that issued them.
+"""Census of the C5 training step's leaf ATen ops (the small torch launches): torch.profiler over two steps of the
+bench's C5 setup (f16 + loss scaler), counted per op name and, where the profiler recorded a Python stack, the
+innermost package frame (ops issued from the autograd engine's backward thread carry none: "?").
 
     python tools/prof_c5_ops.py [--steps 2] [--top 40]
 """
