@@ -21,9 +21,10 @@ def child(kind):
     from image_compression_2_amd import _native as nv
     dev = torch.device("cuda", 0)
     torch.manual_seed(1)
-    G = ic2.Generator(img_resolution=256, precision="bf16").to(dev)
+    # BK_RES / BK_N: another generator resolution / batch (e.g. 1024 / 8 for the C4 layers)
+    G = ic2.Generator(img_resolution=int(os.environ.get("BK_RES", 256)), precision="bf16").to(dev)
     res = {}
-    n = 32
+    n = int(os.environ.get("BK_N", 32))
     for name in G.synthesis.layer_names[:-1]:
         L = getattr(G.synthesis, name)
         s_in = int(L.in_size[0])
@@ -66,7 +67,11 @@ def child(kind):
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / 10
-        res[name] = (round(ms * 1e3, 1), round(work / (ms * 1e-3) / 1e12, 1) if work else None)
+        if kind == "flr":  # compulsory bytes (f16 in, bf16 out) at the achieved rate, TB/s
+            nbytes = n * (conv * conv + s_out * s_out) * L.cout_p * 2
+            res[name] = (round(ms * 1e3, 1), round(nbytes / (ms * 1e-3) / 1e12, 2))
+        else:
+            res[name] = (round(ms * 1e3, 1), round(work / (ms * 1e-3) / 1e12, 1) if work else None)
     print(json.dumps(res))
 
 
@@ -88,7 +93,7 @@ def main():
             continue
         table[v] = json.loads(r.stdout.strip().splitlines()[-1])
     names = list(next(iter(table.values())).keys()) if table else []
-    print(f"{kind}: us (TFLOP/s) per layer, batch 32 bf16")
+    print(f"{kind}: us ({'TB/s of compulsory bytes' if kind == 'flr' else 'TFLOP/s'}) per layer")
     print(f"{'layer':14s}" + "".join(f"{v[-15:]:>16s}" for v in table))
     for nm in names:
         print(f"{nm:14s}" + "".join(f"{str(table[v][nm]):>16s}" for v in table))
