@@ -511,8 +511,10 @@ static void fbm_launch(FlrBwdMArgs a, int n, hipStream_t s) {
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_bwd_mfma_kernel<U, TJX, GF16>, 512, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
+  // strip segmentation as the forward's (fm_strip_segments); knob IC2_FLRB_SEGS=0 keeps the round-3 rule
+  static const int segs_mode = knob("IC2_FLRB_SEGS", 1);
   const int64_t nstrips = (int64_t)n * a.tiles_x * a.cblocks;
-  int nseg = (int)std::min<int64_t>(a.tiles_y, std::max<int64_t>(1, ceil_div(2 * (int64_t)resident, nstrips)));
+  int nseg = fm_strip_segments(nstrips, a.tiles_y, resident, segs_mode == 1);
   const int seg_len = (int)ceil_div(a.tiles_y, nseg);
   nseg = (int)ceil_div(a.tiles_y, seg_len);
   const int nitems = (int)(nstrips * nseg);

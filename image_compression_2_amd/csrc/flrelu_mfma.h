@@ -57,4 +57,26 @@ __device__ __forceinline__ int fm_xcd_remap(int b, int nblocks) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
 }
 
+// Strip segmentation of the persistent strip kernels (forward flrelu_mfma3, backward flrelu_bwd_mfma): the grid of
+// `resident` workgroups takes the nstrips * nseg items round-robin, so a launch lasts ceil(items / resident) rounds
+// of one item.  Base rule (round 3): whole strips when there are >= 2 per resident workgroup, else the fewest
+// segments that give 2.  `tune`: on strips of <= 40 tiles, the segmentation that minimises rounds x (segment tiles +
+// a per-item start cost of about one tile: the ring prologue and the halo rows above the segment) -- whole strips
+// on 2.1-2.5 items per workgroup idle much of the chip in the last round (SG3-T-1024 L5 / L6 / L8 / L9 -9 / -5 / -11
+// / -15 %, profiles/r4zp_flr_segments_ab.txt); the 1044^2 layers' 66-tile strips measured level to 11 % slower cut.
+inline int fm_strip_segments(int64_t nstrips, int tiles_y, int resident, bool tune) {
+  int64_t nseg = (2 * (int64_t)resident + nstrips - 1) / nstrips;
+  nseg = nseg < 1 ? 1 : (nseg > tiles_y ? tiles_y : nseg);
+  if (tune && tiles_y <= 40) {
+    int64_t best = -1, pick = nseg;
+    for (int64_t sg = nseg; sg <= tiles_y && sg <= nseg + 16; ++sg) {
+      const int64_t len = (tiles_y + sg - 1) / sg, segs = (tiles_y + len - 1) / len;
+      const int64_t cost = (nstrips * segs + resident - 1) / resident * (len + 1);
+      if (best < 0 || cost < best) best = cost, pick = segs;
+    }
+    nseg = pick;
+  }
+  return (int)nseg;
+}
+
 }  // namespace ic2

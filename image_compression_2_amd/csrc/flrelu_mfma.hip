@@ -1150,24 +1150,10 @@ static void fm3_launch_cl(FlrArgs a, int n, hipStream_t s) {
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flrelu_mfma3_kernel<U, DELTA, NW, CL>, 64 * NW, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
-  // the persistent grid takes items round-robin, so the launch lasts ceil(items / resident) rounds of one item:
-  // on strips of <= 40 tiles choose the segmentation that minimises rounds x (segment tiles + a per-item start
-  // cost of about one tile: the ring prologue and the halo rows above the segment).  Whole-height strips on a grid
-  // of 2.1-2.5 items per workgroup idle a large part of the CUs in the last round: SG3-T-1024 L5 / L6 / L8 / L9
-  // -9 / -5 / -11 / -15 %, SG3-T-256 L12 -3 % (profiles/r4zp_flr_segments_ab.txt).  Longer strips stay whole: cut,
-  // the 1044^2 layers measured level to 11 % slower.  Knob IC2_FLR_SEGS=0: the round-3 rule only (whole strips when
-  // there are >= 2 per resident workgroup, else the fewest segments that give 2).
+  // strip segmentation: fm_strip_segments (flrelu_mfma.h); knob IC2_FLR_SEGS=0 keeps the round-3 rule
   static const int segs_mode = knob("IC2_FLR_SEGS", 1);
   const int64_t nstrips = (int64_t)n * a.tiles_x * a.cblocks;
-  int nseg = (int)std::min<int64_t>(a.tiles_y, std::max<int64_t>(1, ceil_div(2 * (int64_t)resident, nstrips)));
-  if (segs_mode == 1 && a.tiles_y <= 40) {
-    int64_t best = -1;
-    for (int s = nseg; s <= a.tiles_y && s <= nseg + 16; ++s) {
-      const int64_t len = ceil_div(a.tiles_y, s), segs = ceil_div(a.tiles_y, len);
-      const int64_t cost = ceil_div(nstrips * segs, (int64_t)resident) * (len + 1);
-      if (best < 0 || cost < best) best = cost, nseg = (int)segs;
-    }
-  }
+  int nseg = fm_strip_segments(nstrips, a.tiles_y, resident, segs_mode == 1);
   const int seg_len = (int)ceil_div(a.tiles_y, nseg);
   nseg = (int)ceil_div(a.tiles_y, seg_len);
   const int nitems = (int)(nstrips * nseg);
