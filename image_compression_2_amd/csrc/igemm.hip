@@ -1095,6 +1095,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 hg4_o128_w32_p2_gn_kernel(IgemmArgs a, int tx, int ty) {
   hg4_body<8, 4, 1, 4, 32, 4, true, false, 2, true>(a, tx, ty);
 }
+// 64-wide outputs on 12 x 32-pixel tiles (wave tile 64 x 96: a weight slab feeds 384 pixels, 1.5x the 8-row tile's)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o64_w32_t12_gn_kernel(IgemmArgs a, int tx, int ty) {
+  hg4_body<4, 6, 1, 4, 32, 4, true, false, 2, true>(a, tx, ty);
+}
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_P
 
@@ -1846,11 +1851,16 @@ static bool x3_gn_hg4(int n, int h, int w_, int cin_p, int cout_p, int cout_vali
   return true;
 }
 
+// rows of the statistics-epilogue kernel's pixel tile: 12 for the 64-wide outputs (knob IC2_X3_GN_T12=0: 8), else 8
+static int x3_gn_th(int cout_p) {
+  static const bool t12 = knob("IC2_X3_GN_T12", 1) != 0;
+  return cout_p == 64 && t12 ? 12 : 8;
+}
 static int64_t x3_gn_part_doubles(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
                                   int groups) {
   if (!x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr)) return 0;
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
-  return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, 8) * 2;  // o64 / o128 w32 tiles: 8 x 32 pixels
+  return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, x3_gn_th(cout_p)) * 2;  // the kernel's 32-wide tiles
 }
 
 bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
@@ -1904,7 +1914,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.x_pix = x_pix_of(IC2_BF16X3, cin_p);
     a.x_hb32 = cin_p / 96;
     const int nc = conv_chunk_n(IC2_BF16X3, n, h, w_, cin_p);
-    const int64_t ntile = ceil_div(wo, 32) * ceil_div(ho, 8);
+    const int64_t ntile = ceil_div(wo, 32) * ceil_div(ho, x3_gn_th(cout_p));
     for (int i0 = 0; i0 < n; i0 += nc) {  // chunks of whole images (< 2^31 input bytes per launch)
       const int cnt = n - i0 < nc ? n - i0 : nc;
       a.x = reinterpret_cast<const char*>(x) + (int64_t)i0 * h * w_ * a.x_pix * 2;
@@ -1912,7 +1922,8 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
       a.gn_part = part + (int64_t)i0 * groups * ntile * 2;
       a.n = cnt;
       a.M = (int)((int64_t)cnt * ho * wo);
-      if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
+      if (p.bo == 64 && x3_gn_th(64) == 12) launch_hg4<4, 6, 1, 4, 32>(a, s, hg4_o64_w32_t12_gn_kernel);
+      else if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
       else launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_p2_gn_kernel);
     }
     return (int)ntile;
