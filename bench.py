@@ -179,7 +179,11 @@ def conv_call_plan(nv, name, args):
     else:
         raise KeyError(name)
     ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
-    return nv.conv_plan(dt, odt, layout, n, h, w, cin_p, cout_p, cv, kh, kw, pad), 2 * n * ho * wo * cout_p * kh * kw * cin_p
+    plan = nv.conv_plan(dt, odt, layout, n, h, w, cin_p, cout_p, cv, kh, kw, pad)
+    if name == "ic2_conv3x3_gn_fwd" and odt == nv.F32 and plan.startswith("hg4_o"):
+        # the split conv with the GroupNorm statistics in its epilogue (igemm.hip x3_gn_hg4: 12-row tiles for 64-wide)
+        plan = "hg4_o64_w32_t12_gn" if plan.startswith("hg4_o64") else plan + "_gn"
+    return plan, 2 * n * ho * wo * cout_p * kh * kw * cin_p
 
 
 def algorithmic_flops_per_image(enc, G, res, split=False):
