@@ -1218,9 +1218,12 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     const int64_t g6 = ceil_div(M, 256) * ((cout_p + 255) / 256), g7 = ceil_div(M, 512) * ((cout_p + 127) / 128);
     const bool k_deep = K / 64 >= 32;
     int g8_split = 1;
+    // knob IC2_G8_TARGET: workgroups the split aims at (default 240, ~1 per CU of the 1-workgroup-per-CU kernel)
+    static const int g8_target = knob("IC2_G8_TARGET", 240);
     if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) tile = 6;
     else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) && g7 >= 240) tile = 7;
-    else if (g8_splitk && splitk && fits8 && k_deep && cout_p > 128 && !odd128) tile = 6, g8_split = (int)ceil_div(240, g6);
+    else if (g8_splitk && splitk && fits8 && k_deep && cout_p > 128 && !odd128)
+      tile = 6, g8_split = (int)ceil_div(g8_target, g6);
     if (g8_split > 1) {
       int64_t sp = g8_split;
       if (sp > K / 64 / 8) sp = K / 64 / 8;  // >= 8 K-tiles of 64 per slice
