@@ -237,6 +237,86 @@ class ToNHWC(torch.autograd.Function):
         return dx, None, None
 
 
+def _synth_layer_grads(L, dt, os_, y, dout):
+    """Backward of one modulated synthesis layer from dL/d(filtered lrelu output) `dout`: the FLR adjoint stored
+    times oscale (dL/dconv) with the per-tile sums for dL/doscale, then the dgrad implicit GEMM -> (dL/da, dL/doscale),
+    a = the conv's (already input-modulated) operand."""
+    n, h, w, c_p = y.shape
+    stream = nv.stream_of(y)
+    _, _, bp = L.packed(dt)
+    fu, fd = L._fu, L._fd
+    px0, px1, py0, py1 = L.padding
+    clamp = float(L.conv_clamp) if L.conv_clamp is not None else -1.0
+    dc = torch.empty([n, h, w, c_p], dtype=dt, device=y.device)
+    rc = 2
+    if fu is not None and fd is not None and px0 == py0:
+        nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, c_p, h, w, L.up_factor))
+        ydot = torch.empty([nyd], dtype=torch.float32, device=y.device)
+        rc = nv.load().ic2_flrelu_bwd_nhwc_ex(
+            nv.ptr(y), nv.dtype_code(y.dtype), nv.ptr(dout), nv.dtype_code(dout.dtype), nv.ptr(dc),
+            nv.dtype_code(dt), n, c_p, h, w, dout.shape[1], dout.shape[2], fu.ctypes.data_as(ctypes.c_void_p),
+            fu.shape[0], fd.ctypes.data_as(ctypes.c_void_p), fd.shape[0], L.up_factor, L.down_factor, px0, px1,
+            py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(os_), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
+        if rc not in (0, 2):
+            raise RuntimeError(f"ic2_flrelu_bwd_nhwc_ex failed: {nv.load().ic2_last_error().decode()}")
+    if rc == 0:
+        yd = ydot.view(n, -1, c_p).sum(1)
+    else:   # no fused instance for this geometry: the composed HIP path + torch epilogue
+        gy = _flrelu_backward_composed(y, dout, L)
+        dc.copy_(gy * os_[:, None, None, :])
+        yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
+    d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
+    # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1)
+    da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0)
+    return da, d_os
+
+
+class SynthLayerScaledNHWC(torch.autograd.Function):
+    """A modulated synthesis layer on the network's training path, taking its input already modulated and
+    returning its output modulated for the NEXT layer (SG3 SynthesisLayer.forward chained):
+        y = conv(a, W_norm) * oscale + bias  ->  out = filtered_lrelu(y) * xs_next
+    The next layer's input modulation rides on this layer's FLR store (its post-scale row, as in inference), so the
+    separate ic2_scale_nhwc pass over every activation is gone.  Backward: dL/d(lrelu out) = g * xs_next and
+    dL/dxs_next = sum_p g * out / xs_next (ic2_scale_bwd_nhwc on the stored, modulated out; 0 where xs_next = 0, where
+    out is 0 too), then _synth_layer_grads; the gradient w.r.t. `a` is dL/da itself."""
+
+    @staticmethod
+    def forward(ctx, a, os_, xs_next, layer, dt):
+        n, s_in = a.shape[0], a.shape[1]
+        a = a.contiguous()
+        assert xs_next.shape == (n, layer.cout_p), (xs_next.shape, layer.cout_p)
+        k = layer.conv_kernel
+        pad = k - 1
+        conv = s_in + 2 * pad - k + 1
+        wp, _, bp = layer.packed(dt)
+        ydt = torch.float16 if dt == torch.bfloat16 else dt
+        y = torch.empty([n, conv, conv, layer.cout_p], dtype=ydt, device=a.device)
+        nv.conv_igemm(nv.ptr(a), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
+                      layer.cin_p, layer.cout_p, layer.out_channels, k, k, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0,
+                      0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(a), a.device)
+        xs32 = xs_next.detach().float().contiguous()
+        out = layer.flrelu_nhwc(y, dt, post_scale=xs32)
+        ctx.save_for_backward(a, os_, xs32, y, out)
+        ctx.layer, ctx.dt = layer, dt
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, os_, xs, y, out = ctx.saved_tensors
+        L, dt = ctx.layer, ctx.dt
+        g = g.to(out.dtype).contiguous()
+        n, ho, wo, c_p = out.shape
+        npart = int(nv.query("ic2_scale_bwd_part_floats", n, ho * wo, c_p))
+        part = torch.empty([npart], dtype=torch.float32, device=out.device)
+        dout = torch.empty_like(out)
+        nv.call("ic2_scale_bwd_nhwc", nv.ptr(g), nv.ptr(out), nv.ptr(xs), nv.ptr(dout), nv.dtype_code(out.dtype), n,
+                ho * wo, c_p, nv.ptr(part), npart, nv.stream_of(out))
+        s = part.view(n, -1, c_p).sum(1)
+        d_xs = torch.where(xs != 0, s / torch.where(xs != 0, xs, torch.ones_like(xs)), torch.zeros_like(xs))
+        da, d_os = _synth_layer_grads(L, dt, os_, y, dout)
+        return da, d_os, d_xs, None, None
+
+
 class ScaleNHWC(torch.autograd.Function):
     """a = x * xscale[n][c] on NHWC (ic2_scale_nhwc), differentiable in x and xscale (ic2_scale_bwd_nhwc: the per-pixel
     sums of d xscale reduce in f32 per chunk, so an f16 activation with a loss-scaled gradient does not overflow the
@@ -388,41 +468,12 @@ class SynthLayerNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, xs, os_, y = ctx.saved_tensors
-        L, dt = ctx.layer, ctx.dt
-        dout = dout.contiguous()
-        n, h, w, c_p = y.shape
-        stream = nv.stream_of(y)
-        _, _, bp = L.packed(dt)
-        fu, fd = L._fu, L._fd
-        px0, px1, py0, py1 = L.padding
-        clamp = float(L.conv_clamp) if L.conv_clamp is not None else -1.0
-        dc = torch.empty([n, h, w, c_p], dtype=dt, device=y.device)
-        rc = 2
-        if fu is not None and fd is not None and px0 == py0:
-            nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, c_p, h, w, L.up_factor))
-            ydot = torch.empty([nyd], dtype=torch.float32, device=y.device)
-            rc = nv.load().ic2_flrelu_bwd_nhwc_ex(
-                nv.ptr(y), nv.dtype_code(y.dtype), nv.ptr(dout), nv.dtype_code(dout.dtype), nv.ptr(dc),
-                nv.dtype_code(dt), n, c_p, h, w, dout.shape[1], dout.shape[2], fu.ctypes.data_as(ctypes.c_void_p),
-                fu.shape[0], fd.ctypes.data_as(ctypes.c_void_p), fd.shape[0], L.up_factor, L.down_factor, px0, px1,
-                py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(os_), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
-            if rc not in (0, 2):
-                raise RuntimeError(f"ic2_flrelu_bwd_nhwc_ex failed: {nv.load().ic2_last_error().decode()}")
-        if rc == 0:
-            yd = ydot.view(n, -1, c_p).sum(1)
-        else:   # no fused instance for this geometry: the composed HIP path + torch epilogue
-            gy = _flrelu_backward_composed(y, dout, L)
-            dc.copy_(gy * os_[:, None, None, :])
-            yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
-        d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
-        # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1)
-        da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0)
-        del dc
-        n_, hi, wi, cin_p = x.shape
+        da, d_os = _synth_layer_grads(ctx.layer, ctx.dt, os_, y, dout.contiguous())
+        n, hi, wi, cin_p = x.shape
         npart = int(nv.query("ic2_scale_bwd_part_floats", n, hi * wi, cin_p))
         part = torch.empty([npart], dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         nv.call("ic2_scale_bwd_nhwc", nv.ptr(da), nv.ptr(x), nv.ptr(xs), nv.ptr(dx), nv.dtype_code(x.dtype), n, hi * wi,
-                cin_p, nv.ptr(part), npart, stream)
+                cin_p, nv.ptr(part), npart, nv.stream_of(y))
         d_xs = part.view(n, -1, cin_p).sum(1)
         return dx, d_xs, d_os, None, None

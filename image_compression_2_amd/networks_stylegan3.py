@@ -483,7 +483,10 @@ class SynthesisLayer(torch.nn.Module):
             return ao.SynthLayerNHWC.apply(x.contiguous(), xs.contiguous(), os_.contiguous(), self, dt)
         # ToRGB (1x1, 3 channels, linear + clamp): input modulation and frozen conv as HIP kernels (the d xscale
         # reduction in f32), the rest as torch ops
-        a = ao.ScaleNHWC.apply(x, xs)
+        return self.torgb_train_nhwc(ao.ScaleNHWC.apply(x, xs), os_, dt, final_scale)
+
+    def torgb_train_nhwc(self, a, os_, dt, final_scale=None):
+        """ToRGB's autograd step on its already-modulated input a NHWC [n, s, s, cin_p] -> NCHW f32 image."""
         wp, _, bp = self.packed(dt)
         c = ao.FrozenConvNHWC.apply(a, wp, self.packed_adjoint(dt), 1, 0, self.out_channels, self.in_channels)
         y = c * os_[:, None, None, :] + bp
@@ -706,12 +709,15 @@ class SynthesisNetwork(torch.nn.Module):
         d = (torch.bmm(s.square(), wsq.transpose(1, 2)) + 1e-8).rsqrt() * igm  # [L, n, om], 0 past cout
         xss = ao.SplitRows.apply(s, tuple(L.cin_p for L in convs))
         oss = ao.SplitRows.apply(d, tuple(L.cout_p for L in convs))
-        for i, L in enumerate(layers):
-            if L.is_torgb:
-                x = L.forward_train_nhwc(x, ws[:, i + 1], dt, final_scale=self.output_scale)
-            else:
-                x = ao.SynthLayerNHWC.apply(x.contiguous(), xss[i], oss[i], L, dt)
-        return x
+        # each layer's input modulation rides on the previous layer's filtered-lrelu store (its post-scale row); the
+        # first layer's on a scale pass, the ToRGB's on the last modulated layer's store
+        rgb = layers[len(convs)]
+        xs_rgb, os_rgb = rgb.modulation_train(ws[:, len(convs) + 1])
+        x = ao.ScaleNHWC.apply(x, xss[0])
+        for i, L in enumerate(convs):
+            xs_next = xss[i + 1] if i + 1 < len(convs) else xs_rgb
+            x = ao.SynthLayerScaledNHWC.apply(x, oss[i], xs_next, L, dt)
+        return rgb.torgb_train_nhwc(x, os_rgb, dt, final_scale=self.output_scale)
 
     def extra_repr(self):
         return "\n".join([
