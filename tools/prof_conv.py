@@ -1,5 +1,5 @@
-"""Run one synthesis-layer implicit-GEMM conv (SG3-T-256 L8 shape by default, batch 32 bf16) a few times:
-the target for rocprofv3 --pmc passes.   python tools/prof_conv.py [cin cout size reps]"""
+"""Run one synthesis-layer implicit-GEMM conv (SG3-T-256 L8 shape by default, batch 32, bf16 or PC_DT=f16) a few
+times: the target for rocprofv3 --pmc passes.   python tools/prof_conv.py [cin cout size reps]"""
 import os
 import sys
 
@@ -14,12 +14,14 @@ def main():
     dev = torch.device("cuda", 0)
     n = 32
     conv = size + 2
-    x = torch.randn(n, size, size, cin, device=dev).to(torch.bfloat16)
-    w = (torch.randn(cout, 3, 3, cin, device=dev) / (9 * cin) ** 0.5).to(torch.bfloat16)
+    dt = torch.float16 if os.environ.get("PC_DT") == "f16" else torch.bfloat16
+    cdt = nv.F16 if dt == torch.float16 else nv.BF16
+    x = torch.randn(n, size, size, cin, device=dev).to(dt)
+    w = (torch.randn(cout, 3, 3, cin, device=dev) / (9 * cin) ** 0.5).to(dt)
     b = torch.zeros(cout, device=dev)
-    y = torch.empty(n, conv, conv, cout, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(n, conv, conv, cout, device=dev, dtype=dt)
     for _ in range(reps):
-        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(w), nv.ptr(y), nv.BF16, nv.BF16, n, size, size, cin, cout, cout,
+        nv.call("ic2_conv_igemm", nv.ptr(x), nv.ptr(w), nv.ptr(y), cdt, cdt, n, size, size, cin, cout, cout,
                 3, 3, 2, conv, conv, None, nv.ptr(b), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(x))
     torch.cuda.synchronize()
     print("ok", float(y.float().abs().mean()))
