@@ -105,8 +105,6 @@ def parse(argv=None):
     ap.add_argument("--no-parity", action="store_true", help="skip the parity record (rank 0, untimed)")
     ap.add_argument("--dry-run", action="store_true", help="CPU / gloo rehearsal of launcher + timing + reductions")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file (rank 0)")
-    ap.add_argument("--train-graph", choices=("auto", "on", "off"), default="off",
-                    help="c5: replay the training step as one captured graph (auto: on for a single process)")
     return ap.parse_args(argv)
 
 
@@ -495,19 +493,15 @@ def run(args):
 
         if train:
             from image_compression_2_amd import training as ict
-            graphed = args.train_graph == "on" or (args.train_graph == "auto" and world == 1)
-            opt = ict.make_optimizer(enc, lr=1e-4, capturable=graphed)
+            opt = ict.make_optimizer(enc, lr=1e-4)
             w_avg = G.mapping.w_avg.view(1, 1, -1)
             # BASELINE config 5 is fp16: the reference's autocast + GradScaler (stylegan3_hvae_full.py:487,669,693-696)
             # as f16 encoder / synthesis with a dynamic loss scaler
             scaler = ict.make_f16(comp) if syn_prec == "f16" else None
-            train_kw = dict(rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01, scaler=scaler)
-            # one process: the whole step (forward, backward, scaler, Adam) captured once and replayed as one graph
-            # (3 untimed capture-warmup steps happen here, before the bench's own warmup)
-            graph_step = ict.GraphedTrainStep(comp, x, opt, w_avg, warmup=3, **train_kw) if graphed else None
 
             def train_step():
-                losses = graph_step() if graphed else ict.train_step(comp, x, opt, w_avg, **train_kw)
+                losses = ict.train_step(comp, x, opt, w_avg, rec_weight=1.0, perceptual_weight=0.0, kl_weight=0.01,
+                                        scaler=scaler)
                 vec = torch.cat([(losses["rec_loss"].double() * batch).view(1),
                                  (losses["kl_loss"].double() * batch).view(1), counts[1:]])
                 return icd.allreduce_sum(vec, device=dev)
@@ -592,8 +586,7 @@ def run(args):
     elif args.config == "c5":
         out["config"].update(quantization_bits=None, loss="rec MSE + 0.01 KL(w_avg); LPIPS excluded (no weights "
                              "offline)", optimizer="Adam(1e-4, (0.9, 0.999))",
-                             parallelism=f"dp{world} (batch-sharded, RCCL gradient all_reduce)",
-                             step_issue="one captured graph replay (GraphedTrainStep)" if graphed else "eager launches")
+                             parallelism=f"dp{world} (batch-sharded, RCCL gradient all_reduce)")
         out["last_step_losses"] = {"rec_loss": round(vec[0].item() / vec[2].item(), 6),
                                    "kl_loss": round(vec[1].item() / vec[2].item(), 4)}
         if syn_prec == "f16":

@@ -471,17 +471,11 @@ class HierarchyProjector(nn.Module):
         self.fc2 = nn.Linear(256, num_ws * w_dim * 2)
 
     fc1_hook = None   # callable(fc1) run after each re-creation (training.train_step: broadcast from rank 0)
-    fc1_device_draw = False   # draw the re-created fc1 on the device generator (training.GraphedTrainStep)
 
     def refresh_fc1(self, in_features, device):
         """Reference quirk (:225-230): a fresh nn.Linear(in_features, 256) on EVERY call whose pooled width differs
-        from in_channels, drawn from the CPU generator; then the hook (data-parallel consistency).  With
-        fc1_device_draw the same initialisation (nn.Linear's kaiming-uniform) runs on the device generator, so a
-        captured graph re-draws fc1 on every replay without a host copy."""
-        if self.fc1_device_draw and device.type == "cuda":
-            self.fc1 = nn.Linear(in_features, 256, device=device)
-        else:
-            self.fc1 = _fresh_linear(in_features, 256, device)
+        from in_channels, drawn from the CPU generator; then the hook (data-parallel consistency)."""
+        self.fc1 = _fresh_linear(in_features, 256, device)
         if self.fc1_hook is not None:
             self.fc1_hook(self.fc1)
 

@@ -39,14 +39,12 @@ def kl_divergence(means, logvars, w_avg):
     return 0.5 * torch.mean(torch.sum(torch.pow(means - w_avg, 2) + torch.exp(logvars) - logvars - 1, dim=[1, 2]))
 
 
-def make_optimizer(encoder, lr=1e-4, capturable=False):
+def make_optimizer(encoder, lr=1e-4):
     """The reference's optimizer (:484), as one fused multi-tensor kernel per step on the device (the same update
-    rule; torch's per-parameter path launched ~8 elementwise kernels per encoder tensor).  ``capturable``: the
-    step may be captured into a graph (GraphedTrainStep; the fused kernel keeps its step count on the device
-    either way)."""
+    rule; torch's per-parameter path launched ~8 elementwise kernels per encoder tensor)."""
     params = list(encoder.parameters())
     fused = all(p.is_cuda for p in params)
-    return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), fused=fused or None, capturable=capturable)
+    return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), fused=fused or None)
 
 
 def make_f16(compressor):
@@ -113,42 +111,3 @@ def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perce
         optimizer.step()
     return {"rec_loss": rec_loss.detach(), "kl_loss": kl.detach(), "perceptual_loss": perceptual.detach(),
             "total_loss": loss.detach()}
-
-
-class GraphedTrainStep:
-    """train_step captured once into a HIP graph and replayed: the ~1450 launches of a step (HIP kernels, the
-    autograd engine's small torch ops, the fused Adam and the loss scaler's device-side overflow check) go to the
-    GPU as one graph launch instead of one host call each, so the step is no longer bound by the host issue rate.
-
-    Single process only (the gradient all_reduce stays eager: use train_step under data parallelism).  ``images``
-    is the static input: copy each new batch into ``step.images`` before calling.  The optimizer must be built
-    with make_optimizer(..., capturable=True).  Differences from eager, by construction of a graph: the fine
-    projector's per-call fc1 (reference quirk :225-230) is drawn on the device generator (same kaiming-uniform
-    initialisation), and the reparameterisation noise comes from the device generator's graph-safe offsets.
-    Returns the same loss dict as train_step; its tensors are overwritten by every replay."""
-
-    def __init__(self, compressor, images, optimizer, w_avg, warmup=3, **kw):
-        if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:
-            raise ValueError("GraphedTrainStep is single-process: use train_step for data parallelism")
-        if not all(g.get("capturable") for g in optimizer.param_groups):
-            raise ValueError("GraphedTrainStep needs make_optimizer(..., capturable=True)")
-        if not images.is_cuda:
-            raise ValueError("GraphedTrainStep needs the batch on the GPU")
-        enc = compressor.encoder
-        for proj in (enc.global_projector, enc.medium_projector, enc.fine_projector):
-            proj.fc1_device_draw = True
-        self.images = images
-        dev = images.device
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):   # warm up off the capture stream (lazy state: scaler, Adam moments)
-            for _ in range(max(1, warmup)):
-                train_step(compressor, images, optimizer, w_avg, sync_gradients=1, **kw)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.losses = train_step(compressor, images, optimizer, w_avg, sync_gradients=1, **kw)
-
-    def __call__(self):
-        self.graph.replay()
-        return self.losses
