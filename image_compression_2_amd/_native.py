@@ -56,6 +56,9 @@ _SIGS = {
     "ic2_conv_igemm_ws_bytes": [_I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_conv_igemm_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F,
                           _I, _P, _I64, _P],
+    "ic2_pack_weight_wino": [_P, _I, _I, _I, _I, _I, _F, _P, _I, _P],
+    "ic2_conv_wino": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I, _P],
+    "ic2_conv_wino_plan": [_I, _I, _I, _I, _I, _I],
     "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "ic2_from_rgb_conv": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
@@ -96,7 +99,7 @@ _SIGS = {
     "ic2_flrelu_bwd_nhwc": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F,
                             _F, _I, _P],
 }
-_RESTYPE = {"ic2_conv_plan": ctypes.c_char_p, "ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
+_RESTYPE = {"ic2_conv_plan": ctypes.c_char_p, "ic2_conv_wino_plan": ctypes.c_char_p, "ic2_conv_igemm_ws_bytes": _I64, "ic2_group_norm_stats_floats": _I64, "ic2_global_avg_pool_floats": _I64,
             "ic2_uint8_sse_scratch_doubles": _I64, "ic2_rc_bound": _I64, "ic2_conv_wgrad_ws_floats": _I64,
             "ic2_gn_lrelu_pool_bwd_floats": _I64, "ic2_conv3x3_gn_stats_floats": _I64,
             "ic2_flrelu_bwd_ydot_floats": _I64, "ic2_scale_bwd_part_floats": _I64}
@@ -163,6 +166,18 @@ def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, k
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=device) if nbytes > 0 else None
     return call("ic2_conv_igemm_ws", x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho,
                 wo, oscale, bias, act, slope, act_gain, clamp, out_mul, out_layout, ptr(ws), nbytes, stream)
+
+
+def wino_plan(n, h, w, cin_p, cout_p, pad):
+    """Name of the ic2_conv_wino instance (tile) for this geometry."""
+    return query("ic2_conv_wino_plan", n, h, w, cin_p, cout_p, pad).decode()
+
+
+def conv_wino(x, u, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, pad, ho, wo, oscale, bias, act, slope,
+              act_gain, clamp, out_mul, out_layout, stream):
+    """ic2_conv_wino: the 3x3 conv as a fused Winograd F(2,3) along x (f16 operands; u from ic2_pack_weight_wino)."""
+    return call("ic2_conv_wino", x, u, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, pad, ho, wo, oscale,
+                bias, act, slope, act_gain, clamp, out_mul, out_layout, stream)
 
 
 _flops_hook = None   # installed by bench.py's instrumented pass: receives each conv's algorithmic FLOPs

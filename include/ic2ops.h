@@ -199,6 +199,23 @@ int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_
                       const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
                       float out_mul, int out_layout, void* workspace, int64_t ws_bytes, void* stream);
 
+/* Winograd F(2,3)-along-x weights for ic2_conv_wino: w[cout][cin][3][3] f32 -> u_out[cout_p][3][4][cin_p] (f16),
+ * U[o][ky][nu][c] = (G w[o][c][ky][:])[nu] * scale (times rsqrt(mean(w^2,[1,2,3])) when prenorm, as
+ * ic2_pack_weight), G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1], zero padded.  Once per weight version. */
+int ic2_pack_weight_wino(const float* w, int cout, int cin, int cout_p, int cin_p, int prenorm, float scale,
+                         void* u_out, int dtype, void* stream);
+
+/* The 3x3 convolution of ic2_conv_igemm (same output / epilogue contract, kh = kw = 3, f16 operands) as a fused
+ * Winograd F(2,3) along x on MFMA: 2/3 of the direct conv's MFMA work; x NHWC f16 [n][h][w][cin_p], u from
+ * ic2_pack_weight_wino.  Replaces the grouped conv2d of modulated_conv2d [SG3-public] on the f16 synthesis path
+ * (stylegan3_hvae_full.py:274,329).  f16 rounding of the transformed input: tools/wino_emu.py. */
+int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, int out_dtype, int n, int h, int w_, int cin_p,
+                  int cout_p, int cout_valid, int pad, int ho, int wo, const float* oscale, const float* bias, int act,
+                  float slope, float act_gain, float clamp, float out_mul, int out_layout, void* stream);
+
+/* ic2_conv_wino's launch plan for a geometry, e.g. "wino_fx_o128_p15x8_f16" (tile: 15 pairs x 8 rows).  Host only. */
+const char* ic2_conv_wino_plan(int n, int h, int w_, int cin_p, int cout_p, int pad);
+
 /* SynthesisInput.forward Fourier features [SG3-public]: t [n][4] = affine(w); per sample the
  * rotation/translation of freqs/phases, the amplitude damping and sin(2*pi*(grid.f + phi)) * amp on a
  * size x size grid -> x_out NHWC [n][size][size][c_p].  (The trailing @ W/sqrt(C) is an ic2_conv_igemm.) */

@@ -1,0 +1,102 @@
+"""ic2_conv_wino (fused Winograd F(2,3) along x, f16 MFMA) against an fp64 conv of the same operands, next to the
+direct f16 implicit GEMM on the same inputs.  Reference: the grouped conv2d of modulated_conv2d [SG3-public] in
+its activation-scaling form (stylegan3_hvae_full.py:274,329), i.e. ic2_conv_igemm's contract for 3x3."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from image_compression_2_amd import _native as nv
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cuda, n, ci, co, s, pad, layout, out_dt, act, seed=0, cin_p=None, cout_p=None):
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    cip = cin_p or nv.pad32(ci)
+    cop = cout_p or nv.pad32(co)
+    ho = s + 2 * pad - 2
+    x = torch.zeros(n, s, s, cip, device=cuda, dtype=torch.float16)
+    x[..., :ci] = torch.randn(n, s, s, ci, device=cuda, generator=g).to(torch.float16)
+    w = torch.randn(co, ci, 3, 3, device=cuda, generator=g)
+    st = nv.stream_of(x)
+    wp = torch.empty(cop, 3, 3, cip, device=cuda, dtype=torch.float16)
+    u = torch.empty(cop, 3, 4, cip, device=cuda, dtype=torch.float16)
+    nv.call("ic2_pack_weight", nv.ptr(w), co, ci, 3, 3, cop, cip, 1, 1.0, nv.ptr(wp), nv.F16, None, st)
+    nv.call("ic2_pack_weight_wino", nv.ptr(w), co, ci, cop, cip, 1, 1.0, nv.ptr(u), nv.F16, st)
+    osc = (torch.rand(n, cop, device=cuda, generator=g) + 0.5) / (9 * ci) ** 0.5
+    bias = torch.randn(cop, device=cuda, generator=g) * 0.1
+    slope, gain, clamp, mul = (0.2, 1.4142135, 2.5, 0.75) if act else (0.0, 1.0, -1.0, 1.0)
+    if layout == nv.NCHW:
+        shape = [n, co, ho, ho]
+    elif layout == nv.NHWC16:
+        shape = [n, cop // 16, ho, ho, 16]
+    else:
+        shape = [n, ho, ho, cop]
+    yd = torch.full(shape, 7.0, device=cuda, dtype=out_dt)
+    yw = torch.full(shape, 7.0, device=cuda, dtype=out_dt)
+    odt = nv.dtype_code(out_dt)
+    nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(yd), nv.F16, odt, n, s, s, cip, cop, co, 3, 3, pad, ho, ho, nv.ptr(osc),
+                  nv.ptr(bias), int(act), slope, gain, clamp, mul, layout, st, cuda)
+    nv.conv_wino(nv.ptr(x), nv.ptr(u), nv.ptr(yw), nv.F16, odt, n, s, s, cip, cop, co, pad, ho, ho, nv.ptr(osc),
+                 nv.ptr(bias), int(act), slope, gain, clamp, mul, layout, st)
+    torch.cuda.synchronize()
+    # fp64 reference: the f16 input, the f32 pre-normalised weights (each kernel rounds its own weights)
+    wn = (w * w.square().mean([1, 2, 3], keepdim=True).rsqrt()).double()
+    xr = x[..., :ci].double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xr, wn, padding=pad) * osc[:, :co, None, None].double() + bias[None, :co, None, None].double()
+    if act:
+        ref = (torch.where(ref < 0, ref * slope, ref) * gain).clamp(-clamp, clamp)
+    ref = ref * mul
+
+    def as_nchw(y):
+        if layout == nv.NCHW:
+            return y.double()
+        if layout == nv.NHWC16:
+            y = y.permute(0, 1, 4, 2, 3).reshape(n, cop, ho, ho)
+        else:
+            y = y.permute(0, 3, 1, 2)
+        return y[:, :co].double()
+    return as_nchw(yd), as_nchw(yw), ref, yw
+
+
+CASES = [  # n, cin, cout, size, pad
+    (2, 32, 32, 9, 2),        # tiny, odd output width (11)
+    (2, 64, 96, 13, 1),       # pad 1, odd output, cout not a multiple of 128
+    (3, 128, 160, 20, 2),     # two o-tiles, the second partial
+    (1, 512, 512, 36, 2),     # SG3-T-256 L0 geometry
+    (2, 96, 64, 33, 0),       # pad 0
+    (2, 256, 384, 52, 2),     # three o-tiles
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_c%d_o%d_s%d_p%d" % c)
+@pytest.mark.parametrize("layout,out_dt,act", [(nv.NHWC16, torch.float16, False), (nv.NHWC, torch.float16, True),
+                                               (nv.NCHW, torch.float32, True), (nv.NHWC, torch.bfloat16, False)],
+                         ids=["nhwc16_f16", "nhwc_f16_act", "nchw_f32_act", "nhwc_bf16"])
+def test_conv_wino_matches_fp64(cuda, case, layout, out_dt, act):
+    n, ci, co, s, pad = case
+    with torch.no_grad():
+        yd, yw, ref, _ = _run(cuda, n, ci, co, s, pad, layout, out_dt, act)
+    yw, yd, ref = yw.cpu(), yd.cpu(), ref.cpu()
+    scale = ref.abs().max().item()
+    e_w = (yw - ref).abs().max().item() / scale
+    e_d = (yd - ref).abs().max().item() / scale
+    # f16 operands: the direct conv's error is the weight / output rounding (~2^-11); the Winograd adds the rounding
+    # of U = G g and of V = B^T d (packed f16 adds) -- bounded at 4x the direct conv's, and absolutely
+    assert e_w < 4e-3 and e_w <= 4 * e_d + 1e-4, (e_w, e_d)
+    assert torch.isfinite(yw).all()
+
+
+def test_conv_wino_leaves_padding_channels_and_bounds(cuda):
+    """Stores stay inside the tensor: the NHWC16 output's padded channel block and nothing past the end is written
+    (the output buffer is pre-filled with 7; padded output channels carry bias 0 * acc = the bias of a zero row)."""
+    with torch.no_grad():
+        _, _, _, yw = _run(cuda, 2, 64, 40, 17, 2, nv.NHWC16, torch.float16, False, cout_p=64)
+    # cout 40 -> padded channels 40..63 hold acc 0 * oscale + bias (the kernel writes every channel < cout_p)
+    assert torch.isfinite(yw).all()
+
+
+def test_conv_wino_plan_names_a_tile(cuda):
+    for s in (36, 52, 84, 148, 276):
+        name = nv.wino_plan(32, s, s, 512, 512, 2)
+        assert name.startswith("wino_fx_o128_p") and name.endswith("_f16"), name
