@@ -87,7 +87,7 @@ HBM_PEAK_GBS = 8000.0
 N_CODES = 256               # 8-bit codes: the record's histogram width
 
 CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gnin_gn_fwd", "ic2_from_rgb_conv",
-                "ic2_from_rgb_conv_x3")
+                "ic2_from_rgb_conv_x3", "ic2_conv_wino")
 TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad",)
 FLR_ENTRIES = ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16")
 
@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-images", type=int, default=3, help="0 disables the CPU baseline leg")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity record (rank 0, untimed)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the untimed secondary C4 entry of the default c2 line (rank 0, N=1)")
     ap.add_argument("--dry-run", action="store_true", help="CPU / gloo rehearsal of launcher + timing + reductions")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file (rank 0)")
     return ap.parse_args(argv)
@@ -176,6 +178,11 @@ def conv_call_plan(nv, name, args):
     elif name == "ic2_conv_wgrad":
         dt, (n, h, w, cin_p, cout_p, kh, kw, pad) = args[3], args[4:12]
         return "conv_wgrad", 2 * n * h * w * cout_p * kh * kw * cin_p
+    elif name == "ic2_conv_wino":
+        # Winograd F(2,3) along x: 4 positions x 3 kernel rows = 12 MFMA products per output pair (the direct conv's
+        # 18); executed = those products over the padded channels and every output pair
+        n, h, w, cin_p, cout_p, cv, pad, ho, wo = args[5:14]
+        return nv.wino_plan(n, h, w, cin_p, cout_p, pad), 2 * n * ho * ((wo + 1) // 2) * cout_p * 12 * cin_p
     else:
         raise KeyError(name)
     ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
@@ -284,6 +291,29 @@ def flr_work_per_image(G):
         byts += b
         bound += max(f / (F32_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9))
     return flops, byts, bound
+
+
+def plan_kernel_tags(plan):
+    """Substrings of the kernel function names a launch-plan instance (ic2_conv_plan / ic2_conv_wino_plan names, as
+    roofline.per_kernel lists them) dispatches -- to check a committed PMC record against the current plan."""
+    p = plan[:-4] if plan.endswith("_f16") else plan
+    if p.startswith("wino_fx"):
+        return ["wino_fx"]
+    if p.startswith("igemm8_og2+og1"):
+        return ["igemm8_og2", "igemm8_og1"]
+    if p.startswith("igemm8_"):
+        return [p.replace("_splitk", "")]
+    if p.startswith("igemm_"):
+        return ["igemm_kernel"]
+    if p.startswith("hg4_"):
+        return [p]
+    if p.startswith("hconv"):
+        return ["hconv_kernel"]
+    if p == "torgb":
+        return ["torgb_kernel"]
+    if p.startswith("from_rgb"):
+        return ["from_rgb_kernel"]
+    return [p]
 
 
 def pmc_traffic(config, precision, batch):
@@ -607,6 +637,9 @@ def run(args):
     if not dry and rank == 0 and not args.no_parity and args.config in ("c2", "c2g", "c4"):
         out["parity"] = parity_record(args, comp, enc, G, x, x_host, res, syn_prec)
 
+    if not dry and rank == 0 and world == 1 and args.config == "c2" and not args.no_secondary:
+        out["secondary"] = {"c4": secondary_c4(args, dev, sync)}
+
     if rank == 0 and world == 1 and args.cpu_baseline_images > 0 and not dry:
         if args.config == "c5":
             out["cpu_baseline"] = cpu_baseline_train(res, gen_res, 1)
@@ -622,6 +655,43 @@ def run(args):
                 f.write(line + "\n")
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def secondary_c4(args, dev, sync, steps=10, warmup=3):
+    """BASELINE config 4 (batch 8, 1024^2, SG3-T-1024) measured after the headline run, on rank 0 at N=1, so the
+    driver's default line carries it: the same step as `--config c4` (encode -> 8-bit quantize -> synthesis -> uint8
+    SSE; the code record and metric all_reduce, a few microseconds, left out), HIP events around each of `steps`
+    steps after `warmup`, and its parity record.  Not part of `value`."""
+    import image_compression_2_amd as ic2
+    from image_compression_2_amd import metrics as icm
+    res, gen_res, batch, desc = CONFIGS["c4"]
+    enc_prec, syn_prec = PRECISIONS[args.precision]
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision=enc_prec).to(dev).eval().requires_grad_(False)
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=gen_res, precision=syn_prec).to(dev).eval()
+    comp = ic2.StyleGAN3Compressor(enc, G)
+    x_host = torch.rand(batch, 3, res, res, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+    x = x_host.to(dev)
+
+    def step():
+        torch.manual_seed(5)
+        with torch.no_grad():
+            q = comp.compress(x, quantization_bits=8, deterministic=True)
+            img = comp.decompress(q)
+            return icm.uint8_sse(img, x)
+    for _ in range(warmup):
+        step()
+    _, elapsed, per = timed_loop(step, steps, sync, lambda: None, use_events=True)
+    rec = {"workload": desc, "value": round(batch * steps / elapsed, 3), "unit": "images/s",
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "ms_per_step_median": round(statistics.median(per), 3),
+           "steps": steps, "warmup": warmup,
+           "note": "untimed w.r.t. the headline value: measured after it, same protocol on one GPU"}
+    if not args.no_parity:
+        ns = argparse.Namespace(**vars(args))
+        ns.config = "c4"
+        rec["parity"] = parity_record(ns, comp, enc, G, x, x_host, res, syn_prec)
+    return rec
 
 
 PARITY_FIXTURE = os.path.join(ROOT, "tests", "golden", "parity_means.npz")
@@ -754,6 +824,12 @@ def roofline(args, nv, step, sync, barrier, enc, G, res, batch, img_s_per_gpu, e
                       "executed_achieved": round(d[3] / (d[1] * 1e-3) / 1e12, 2),
                       "frac": round(d[2] / (d[1] * 1e-3) / 1e12 / peak, 4) if d[2] else None,
                       "executed_frac": round(d[3] / (d[1] * 1e-3) / 1e12 / peak, 4)}
+    if dom_plan.startswith("wino"):
+        # a Winograd instance issues 2/3 of the direct conv's MFMA FLOPs: its roofline fraction is the executed
+        # (MFMA-issued) one, <= 1; the algorithmic (direct-conv FLOPs) figure stays beside it
+        dm = rl["dominant"]
+        dm["frac_algorithmic"], dm["frac"] = dm["frac"], dm["executed_frac"]
+        dm["achieved_algorithmic"], dm["achieved"] = dm["achieved"], dm["executed_achieved"]
     rl["per_kernel"] = {k: {"launches_per_step": round(v[0] / n_inst, 2), "ms_per_step": round(v[1] / n_inst, 3),
                             "alg_tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[2] else None,
                             "executed_tflops": round(v[3] / (v[1] * 1e-3) / 1e12, 1)}
@@ -766,9 +842,17 @@ def roofline(args, nv, step, sync, barrier, enc, G, res, batch, img_s_per_gpu, e
             (algorithmic_bytes_per_image(enc, G, res, esz, enc_split=split) * batch + wb) / n_conv)
         pm = pmc_traffic(args.config, args.precision, batch)
         if pm is not None:
-            rl["traffic"] = pm["hbm_bytes_per_launch"]
-            rl["traffic_unit"] = "bytes/launch"
+            # the committed PMC run describes the code it ran: its dispatch names must cover every kernel instance
+            # the current launch plan runs, else the figure is from an earlier build and is reported as stale
+            names = list(pm.get("dispatches", {}))
+            missing = sorted({t for plan in per for t in plan_kernel_tags(plan) if not any(t in d for d in names)})
             rl["traffic_src"] = pm["src"]
+            rl["traffic_unit"] = "bytes/launch"
+            if missing:
+                rl["traffic_stale"] = {"pmc_bytes_per_launch": pm["hbm_bytes_per_launch"],
+                                       "kernels_not_in_pmc_run": missing}
+            else:
+                rl["traffic"] = pm["hbm_bytes_per_launch"]
     flr_calls = timer.calls(FLR_ENTRIES)
     if syn_prec in ("bf16", "f16") and flr_calls and not train:
         flr_ms = sum(c[3] for c in flr_calls)

@@ -59,6 +59,8 @@ _SIGS = {
     "ic2_pack_weight_wino": [_P, _I, _I, _I, _I, _I, _F, _P, _I, _P],
     "ic2_conv_wino": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I, _P],
     "ic2_conv_wino_plan": [_I, _I, _I, _I, _I, _I],
+    "ic2_conv_wino_preferred": [_I, _I, _I, _I, _I, _I, _I, _I, _I],
+    "ic2_conv_wino_stamps": [_P, _I64],
     "ic2_synth_input_features": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _P, _I, _P],
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "ic2_from_rgb_conv": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
@@ -166,6 +168,11 @@ def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, k
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=device) if nbytes > 0 else None
     return call("ic2_conv_igemm_ws", x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho,
                 wo, oscale, bias, act, slope, act_gain, clamp, out_mul, out_layout, ptr(ws), nbytes, stream)
+
+
+def wino_preferred(dtype, n, h, w, cin_p, cout_p, kh, kw, pad):
+    """True when the library's launch plan runs this conv as the Winograd kernel (ic2_conv_wino)."""
+    return bool(query("ic2_conv_wino_preferred", dtype, n, h, w, cin_p, cout_p, kh, kw, pad))
 
 
 def wino_plan(n, h, w, cin_p, cout_p, pad):

@@ -70,6 +70,17 @@ __device__ __forceinline__ int wx_hoff(int line, int hp, int idx, int chunk) {
 #ifndef IC2_WX_ABL
 #define IC2_WX_ABL 0
 #endif
+// diagnostic build IC2_WX_STAMP=1 (tools/build_abl.sh winostamp): s_memtime stamps around the sections, summed per
+// wave over the K loop and stored to a.ws[(block * 8 + wave) * 8 + k] as u64 (the launch passes a buffer there):
+// 0 R reads + V, 1 R DMA issue, 2 vmcnt wait, 3 barrier after R + lgkmcnt, 4 M issue, 5 barrier after M, 6 loop
+#ifndef IC2_WX_STAMP
+#define IC2_WX_STAMP 0
+#endif
+// schedule variants (A/B): 0 = reads, V, then DMAs in R; 1 = DMAs first in R; 2 = DMAs first, and the next step's
+// input fragments read inside the second M section of the step (halo DMAs one section later to keep the WAR distance)
+#ifndef IC2_WX_SCHED
+#define IC2_WX_SCHED 0
+#endif
 
 __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[WX_LDS];
@@ -82,9 +93,13 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
   const int pg = wid & 3;     // pairs 32 pg .. 32 pg + 31
   const int fr = lane & 15, fh = lane >> 4;
 
+  // logical tile -> (o-tile, pixel tile): the o-tiles run in groups of a.group (fastest within a group), each group
+  // over all pixel tiles; the XCD remap hands every XCD a contiguous range, so its L2 holds the U slabs of one group
   const int logical = xcd_remap(blockIdx.x, a.nblocks);
-  const int o_tile = logical % a.tiles_o;
-  int pt = logical / a.tiles_o;
+  const int per_group = a.group * (a.nblocks / a.tiles_o);
+  const int gi = logical / per_group, grem = logical - gi * per_group;
+  const int o_tile = gi * a.group + grem % a.group;
+  int pt = grem / a.group;
   const int tx = pt % a.wx_tx;
   pt /= a.wx_tx;
   const int ty = pt % a.wx_ty;
@@ -208,13 +223,27 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
 #pragma unroll
   for (int j = 0; j < 5; ++j) issue_hs(0, j);
   issue_hp(1, 0);
-  issue_hp(1, 1);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // halo 0, half-slabs 0-2 landed (3, 4, halo 1 p0-1 in flight)
+  if constexpr (IC2_WX_SCHED == 2) {
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // halo 0, half-slabs 0-2 landed (3, 4, halo 1 p0 in flight)
+  } else {
+    issue_hp(1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // halo 0, half-slabs 0-2 landed (3, 4, halo 1 p0-1 in flight)
+  }
   __builtin_amdgcn_s_barrier();
   read_d(hal);
   if (half == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 run one barrier behind
   __builtin_amdgcn_sched_barrier(0);
 
+  uint64_t st[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t t_prev = 0, t_loop = 0;
+  auto stamp = [&](int k) {
+    if constexpr (IC2_WX_STAMP) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      st[k] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  if constexpr (IC2_WX_STAMP) t_loop = t_prev = __builtin_amdgcn_s_memtime();
   for (int cb = 0; cb < CB; ++cb) {
     const char* hb_cur = hal + (cb & 1) * WX_HALO;
     const char* hb_nxt = hal + ((cb + 1) & 1) * WX_HALO;
@@ -224,31 +253,55 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
       const char* wl = wsl + j * (WX_SLAB / 2) + aoff;
       bf16x8 af[2][4];
       // ---- R section
+      auto r_dma = [&]() {
+        if (!(IC2_WX_ABL & 1) || cb == 0) issue_hs(cb + (j + 5) / 6, (j + 5) % 6);
+        if constexpr (IC2_WX_SCHED == 2) {
+          if (j == 0) issue_hp(cb + 1, 1);
+          if (j == 1) issue_hp(cb + 1, 2);
+          if (j == 5) issue_hp(cb + 2, 0);
+        } else {
+          if (j == 0) issue_hp(cb + 1, 2);
+          if (j >= 4) issue_hp(cb + 2, j - 4);
+        }
+      };
+      if constexpr (IC2_WX_SCHED >= 1) r_dma();
       if (hx == 0) make_v();
 #pragma unroll
       for (int nl = 0; nl < 2; ++nl)
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[nl][i] = *reinterpret_cast<const bf16x8*>(wl + (nl * 64 + i * 16) * 64);
-      if (hx == 1) {
+      if (hx == 1 && IC2_WX_SCHED < 2) {
         if constexpr (!(IC2_WX_ABL & 4)) read_d(ky < 2 ? hb_cur + (ky + 1) * ky_step : hb_nxt);
       }
-      if (!(IC2_WX_ABL & 1) || cb == 0) issue_hs(cb + (j + 5) / 6, (j + 5) % 6);
-      if (j == 0) issue_hp(cb + 1, 2);
-      if (j >= 4) issue_hp(cb + 2, j - 4);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(IC2_WX_ABL & 16)) {
-        if (j == 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        if (j == 1 || j == 5) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        if (j == 2 || j == 4) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        if (j == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (IC2_WX_STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp(0);
       }
+      if constexpr (IC2_WX_SCHED == 0) r_dma();
+      __builtin_amdgcn_sched_barrier(0);
+      stamp(1);
+      if constexpr (!(IC2_WX_ABL & 16)) {
+        if constexpr (IC2_WX_SCHED == 2) {  // halo DMAs at sections 5, 0, 1: 8 9 8 7 6 7
+          if (j == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+          if (j == 0 || j == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if (j == 3 || j == 5) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+          if (j == 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          if (j == 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+          if (j == 1 || j == 5) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if (j == 2 || j == 4) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+          if (j == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        }
+      }
+      stamp(2);
       if constexpr (!(IC2_WX_ABL & 2)) __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      stamp(3);
       // ---- M section
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int nl = 0; nl < 2; ++nl)
+      for (int nl = 0; nl < 2; ++nl) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -258,10 +311,29 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
               acc[nl][4 * hx + i][jb] =
                   mfma32<true>(af[nl][i], __builtin_bit_cast(bf16x8, v[nl][jb]), acc[nl][4 * hx + i][jb]);
           }
+        if (IC2_WX_SCHED == 2 && hx == 1 && nl == 0) {  // the next step's input fragments behind the MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!(IC2_WX_ABL & 4)) read_d(ky < 2 ? hb_cur + (ky + 1) * ky_step : hb_nxt);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (IC2_WX_STAMP) {  // the MFMAs issued (the last one still in the pipe)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      stamp(4);
       if constexpr (!(IC2_WX_ABL & 2)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      stamp(5);
+    }
+  }
+  if constexpr (IC2_WX_STAMP) {
+    st[6] = __builtin_amdgcn_s_memtime() - t_loop;
+    if (lane == 0) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(a.ws) + ((int64_t)blockIdx.x * 8 + wid) * 8;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) o[k] = st[k];
     }
   }
   if (half == 0) __builtin_amdgcn_s_barrier();  // balance the waves 4-7 offset barrier
@@ -422,9 +494,19 @@ static int wx_chunk_n(int n, int h, int w_, int cin_p) {
   return (int)ceil_div(n, ceil_div(n, c));
 }
 
+static void* g_wx_stamp = nullptr;  // diagnostic stamp buffer (IC2_WX_STAMP builds)
+static int64_t g_wx_stamp_bytes = 0;
+
 }  // namespace ic2
 
 using namespace ic2;
+
+extern "C" int ic2_conv_wino_stamps(void* buf, int64_t bytes) {
+  IC2_CHECK_ARG(IC2_WX_STAMP, "conv_wino_stamps: not a stamp build (IC2_WX_STAMP)");
+  g_wx_stamp = buf;
+  g_wx_stamp_bytes = bytes;
+  return IC2_OK;
+}
 
 extern "C" int ic2_pack_weight_wino(const float* w, int cout, int cin, int cout_p, int cin_p, int prenorm,
                                     float scale, void* u_out, int dtype, void* stream) {
@@ -434,6 +516,20 @@ extern "C" int ic2_pack_weight_wino(const float* w, int cout, int cin, int cout_
                      prenorm, scale, (_Float16*)u_out);
   IC2_CHECK_LAUNCH("pack_weight_wino");
   return IC2_OK;
+}
+
+// Where the Winograd kernel beats the direct implicit GEMM (tools/bench_wino.py, f16 at batch 32): the >= 256-wide
+// convs on >= 50-pixel outputs (SG3-T-256 L4-L10: 1.10-1.18x); the 38-pixel L0-L3 (tiles pad the 19-pair rows) and
+// the <= 192-wide L11-L13 (hg4) stay direct.  IC2_WINO=0 / 2 (dev knob): never / wherever legal.
+extern "C" int ic2_conv_wino_preferred(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw,
+                                       int pad) {
+  static const int mode = knob("IC2_WINO", 1);
+  const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
+  const bool legal = dtype == IC2_F16 && kh == 3 && kw == 3 && n > 0 && ho > 0 && wo > 0 && cin_p % 32 == 0 &&
+                     cout_p % 32 == 0 && (int64_t)cout_p * 12 * cin_p * 2 < (int64_t)kOob;
+  if (!legal || mode == 0) return 0;
+  if (mode == 2) return 1;
+  return cin_p >= 256 && cout_p >= 256 && ho >= 50 && wo >= 50;
 }
 
 extern "C" const char* ic2_conv_wino_plan(int n, int h, int w_, int cin_p, int cout_p, int pad) {
@@ -481,11 +577,19 @@ extern "C" int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, i
   const WxTile t = wx_tile(n, ho, wo, cout_p);
   IC2_CHECK_ARG(t.blocks > 0 && t.blocks < (1LL << 31), "conv_wino: bad tile plan");
   IgemmArgs a{};
-  a.x = x; a.w = u; a.y = y; a.oscale = oscale; a.bias = bias; a.ws = nullptr;
+  a.x = x; a.w = u; a.y = y; a.oscale = oscale; a.bias = bias;
+  a.ws = IC2_WX_STAMP && (int64_t)t.blocks * 8 * 8 * 8 <= g_wx_stamp_bytes ? reinterpret_cast<float*>(g_wx_stamp)
+                                                                          : nullptr;
+  IC2_CHECK_ARG(!IC2_WX_STAMP || a.ws, "conv_wino: stamp build without a large enough ic2_conv_wino_stamps buffer");
   a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
   a.kh = 3; a.kw = 3; a.pad = pad; a.ho = ho; a.wo = wo;
   a.M = n * ho * wo; a.K = 9 * cin_p; a.nq = 3 * (cin_p / 32);
-  a.tiles_o = t.to; a.nblocks = (int)t.blocks; a.group = 1; a.korder = 1; a.o_base = 0;
+  // o-tiles per L2 group (1: each XCD streams one o-tile's U, 1.5 MiB at 512 channels; the input halos are read by
+  // tiles_o XCDs instead of one)
+  static const int og_knob = knob("IC2_WINO_OGROUP", 1);
+  int og = og_knob < 1 ? 1 : og_knob > t.to ? t.to : og_knob;
+  while (t.to % og) --og;
+  a.tiles_o = t.to; a.nblocks = (int)t.blocks; a.group = og; a.korder = 1; a.o_base = 0;
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
   a.out_layout = out_layout; a.out_dtype = out_dtype;
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0; a.in_gn = nullptr; a.in_slope = 0.f;

@@ -419,10 +419,31 @@ class SynthesisLayer(torch.nn.Module):
             y = torch.empty([n, self.cout_p // 16, conv, conv, 16], dtype=ydt, device=x.device)
         else:
             y = torch.empty([n, conv, conv, self.cout_p], dtype=ydt, device=x.device)
-        nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
-                      self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
-                      0.0, 1.0, -1.0, 1.0, nv.NHWC16 if blocked else nv.NHWC, stream, x.device)
+        layout = nv.NHWC16 if blocked else nv.NHWC
+        if nv.wino_preferred(nv.dtype_code(dt), n, s_in, s_in, self.cin_p, self.cout_p, k, k, pad):
+            # f16, >= 256 channels: the fused Winograd F(2,3)-along-x kernel (2/3 of the MFMA work, wino.hip)
+            nv.conv_wino(nv.ptr(x), nv.ptr(self.packed_wino()), nv.ptr(y), nv.F16, nv.dtype_code(ydt), n, s_in, s_in,
+                         self.cin_p, self.cout_p, self.out_channels, pad, conv, conv, nv.ptr(oscale), nv.ptr(bp), 0,
+                         0.0, 1.0, -1.0, 1.0, layout, stream)
+        else:
+            nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
+                          self.cin_p, self.cout_p, self.out_channels, k, k, pad, conv, conv, nv.ptr(oscale),
+                          nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, layout, stream, x.device)
         return y, blocked
+
+    def packed_wino(self):
+        """Winograd F(2,3)-along-x weights U [cout_p][3][4][cin_p] f16 of the pre-normalised W, per weight version
+        (ic2_pack_weight_wino, from the f32 master weights: one rounding)."""
+        key = _version_key(self.weight)
+        hit = self._cache.get("wino")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w = self.weight.detach().to(torch.float32).contiguous()
+        u = torch.empty([self.cout_p, 3, 4, self.cin_p], dtype=torch.float16, device=w.device)
+        nv.call("ic2_pack_weight_wino", nv.ptr(w), self.out_channels, self.in_channels, self.cout_p, self.cin_p,
+                int(not self.is_torgb), 1.0, nv.ptr(u), nv.F16, nv.stream_of(w))
+        self._cache["wino"] = (key, u)
+        return u
 
     def flrelu_nhwc(self, y, dt_out, post_scale=None, blocked=False):
         """The layer's filtered lrelu on the conv output y NHWC [n, conv, conv, cout_p] (f32, or f16 for the

@@ -213,6 +213,14 @@ int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, int out_dtyp
                   int cout_p, int cout_valid, int pad, int ho, int wo, const float* oscale, const float* bias, int act,
                   float slope, float act_gain, float clamp, float out_mul, int out_layout, void* stream);
 
+/* 1 when the library's launch plan runs this 3x3 conv as ic2_conv_wino (f16 operands, a geometry where it beats the
+ * direct implicit GEMM), else 0.  Host only. */
+int ic2_conv_wino_preferred(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad);
+
+/* Diagnostic builds only (IC2_WX_STAMP, tools/build_abl.sh winostamp): a device buffer for ic2_conv_wino's per-wave
+ * section timestamps (u64 [blocks][8 waves][8]); IC2_E_INVALID in the product build. */
+int ic2_conv_wino_stamps(void* buf, int64_t bytes);
+
 /* ic2_conv_wino's launch plan for a geometry, e.g. "wino_fx_o128_p15x8_f16" (tile: 15 pairs x 8 rows).  Host only. */
 const char* ic2_conv_wino_plan(int n, int h, int w_, int cin_p, int cout_p, int pad);
 

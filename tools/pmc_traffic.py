@@ -8,7 +8,7 @@ streaming read on gfx950 (the operand loads are 16-B-per-lane LDS-DMA), so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 Families (round 3: the same launch set bench.py's roofline times):
   conv  -- every dispatch behind a conv entry point (igemm*, the split-K combine, hg4, the halo conv, ToRGB,
-           from_rgb); per launch = bytes / conv-body dispatches (the split 384-wide layer's og2 + og1 pair and the
+           from_rgb, the Winograd conv); per launch = bytes / conv-body dispatches (the split 384-wide layer's og2 + og1 pair and the
            split-K combine count as one launch), matching bench.py's per-call accounting;
   igemm8_og2 -- the dominant kernel alone (per dispatch; the og2 half of a split 384 pair included);
   flr   -- the fused filtered lrelu (flrelu_mfma*), per dispatch.
@@ -19,7 +19,7 @@ import glob
 import json
 import sys
 
-CONV = ("igemm", "hg4_", "hconv_kernel", "torgb_kernel", "from_rgb_kernel")
+CONV = ("igemm", "hg4_", "hconv_kernel", "torgb_kernel", "from_rgb_kernel", "wino_fx")
 
 
 def main():
