@@ -162,8 +162,9 @@ def conv_plan(dtype, out_dtype, out_layout, n, h, w, cin_p, cout_p, cout_valid, 
 
 def conv_igemm(x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo, oscale, bias,
                act, slope, act_gain, clamp, out_mul, out_layout, stream, device):
-    """ic2_conv_igemm with the split-K workspace the launch plan asks for (a stream-ordered torch
-    allocation, so the call stays capturable in a hipGraph)."""
+    """ic2_conv_igemm with the split-K workspace the launch plan asks for (a stream-ordered torch allocation: the
+    call allocates nothing else and never synchronises the host).  Whole-step capture of the f16 training step is not
+    part of the product (training.py: its round-4 trial replayed a negative rec_loss, see DESIGN.md Training)."""
     nbytes = int(query("ic2_conv_igemm_ws_bytes", dtype, n, h, w_, cin_p, cout_p, kh, kw, pad))
     ws = torch.empty([max(nbytes, 16) // 4], dtype=torch.float32, device=device) if nbytes > 0 else None
     return call("ic2_conv_igemm_ws", x, w, y, dtype, out_dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho,

@@ -346,8 +346,11 @@ extern "C" int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* go
   if ((mfma || gf16) && x_dtype == IC2_F16 && ((g_dtype == IC2_BF16 && gx_dtype == IC2_BF16) || gf16)) {
     const int64_t need = (int64_t)n * ceil_div(in_h, 16) * ceil_div(in_w, 16) * c_p;
     IC2_CHECK_ARG(ydot == nullptr || ydot_floats >= need, "flrelu_bwd_nhwc: ydot needs %lld floats", (long long)need);
-    // U is recomputed with the forward's f16 taps: the same joint per-phase rounding, so the lrelu side
-    // and the clamp are decided on the forward's vertical operands
+    // U is recomputed with f16 taps rounded as the forward rounds its vertical taps (joint per-phase rounding, ADVICE
+    // r3), so the lrelu side is decided on the forward's operands.  With a finite clamp the forward's horizontal up pass
+    // runs on separately rounded taps gu / lim (its clamp-split activation, flrelu_mfma.hip) and compares with 1, so an
+    // element within an f16 rounding of the clamp boundary can take the other clamp decision here than in the forward
+    // (its gradient is then 0 instead of gain, or the reverse) -- ADVICE r4; elsewhere the decisions agree.
     float gur[24] = {}, gdr[12] = {};
     f16_round_taps(a.gu, gur, fu_taps, up);
     f16_round_taps(a.gd, gdr, fd_taps, 1);
