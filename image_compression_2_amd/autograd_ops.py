@@ -96,12 +96,19 @@ class SplitRows(torch.autograd.Function):
         return g, None
 
 
-def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None):
+def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None, wino=None):
+    """Conv on NHWC x with packed weights wp [cout_p][kh][kh][cin_p].  wino: a callable returning the same weights
+    packed for the Winograd kernel (U [cout_p][3][4][cin_p] f16), used where ic2_conv_wino_preferred picks it."""
     n, h, w, cin_p = x.shape
     cout_p = wp.shape[0]
     ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kh + 1
     dt_out = x.dtype if dt_out is None else dt_out
     y = torch.empty([n, ho, wo, cout_p], dtype=dt_out, device=x.device)
+    if wino is not None and nv.wino_preferred(nv.dtype_code(x.dtype), n, h, w, cin_p, cout_p, kh, kh, pad):
+        nv.conv_wino(nv.ptr(x), nv.ptr(wino()), nv.ptr(y), nv.dtype_code(x.dtype), nv.dtype_code(dt_out), n, h, w,
+                     cin_p, cout_p, cout_valid, pad, ho, wo, None, nv.ptr(bias_p), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
+                     nv.stream_of(x))
+        return y
     nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.dtype), nv.dtype_code(dt_out), n, h, w, cin_p,
                   cout_p, cout_valid, kh, kh, pad, ho, wo, None, nv.ptr(bias_p), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
                   nv.stream_of(x), x.device)
@@ -267,8 +274,27 @@ def _synth_layer_grads(L, dt, os_, y, dout):
         yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
     d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
     # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1)
-    da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0)
+    da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0,
+                   wino=L.packed_adjoint_wino if dt == torch.float16 else None)
     return da, d_os
+
+
+def _synth_conv_fwd(layer, a, os_, dt, y):
+    """The modulated conv of the training forward: y = conv(a, W_norm) * oscale + bias, NHWC (f16 operands: the
+    Winograd kernel where ic2_conv_wino_preferred picks it, as inference's conv_nhwc)."""
+    n, s_in = a.shape[0], a.shape[1]
+    k = layer.conv_kernel
+    pad = k - 1
+    conv = y.shape[1]
+    wp, _, bp = layer.packed(dt)
+    if dt == torch.float16 and nv.wino_preferred(nv.F16, n, s_in, s_in, layer.cin_p, layer.cout_p, k, k, pad):
+        nv.conv_wino(nv.ptr(a), nv.ptr(layer.packed_wino()), nv.ptr(y), nv.F16, nv.dtype_code(y.dtype), n, s_in, s_in,
+                     layer.cin_p, layer.cout_p, layer.out_channels, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0, 0.0,
+                     1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(a))
+        return
+    nv.conv_igemm(nv.ptr(a), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(y.dtype), n, s_in, s_in,
+                  layer.cin_p, layer.cout_p, layer.out_channels, k, k, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0,
+                  0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(a), a.device)
 
 
 class SynthLayerScaledNHWC(torch.autograd.Function):
@@ -288,12 +314,9 @@ class SynthLayerScaledNHWC(torch.autograd.Function):
         k = layer.conv_kernel
         pad = k - 1
         conv = s_in + 2 * pad - k + 1
-        wp, _, bp = layer.packed(dt)
         ydt = torch.float16 if dt == torch.bfloat16 else dt
         y = torch.empty([n, conv, conv, layer.cout_p], dtype=ydt, device=a.device)
-        nv.conv_igemm(nv.ptr(a), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
-                      layer.cin_p, layer.cout_p, layer.out_channels, k, k, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0,
-                      0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(a), a.device)
+        _synth_conv_fwd(layer, a, os_, dt, y)
         xs32 = xs_next.detach().float().contiguous()
         out = layer.flrelu_nhwc(y, dt, post_scale=xs32)
         ctx.save_for_backward(a, os_, xs32, y, out)
@@ -453,12 +476,9 @@ class SynthLayerNHWC(torch.autograd.Function):
         k = layer.conv_kernel
         pad = k - 1
         conv = s_in + 2 * pad - k + 1
-        wp, _, bp = layer.packed(dt)
         ydt = torch.float16 if dt == torch.bfloat16 else dt
         y = torch.empty([n, conv, conv, layer.cout_p], dtype=ydt, device=x.device)
-        nv.conv_igemm(nv.ptr(a), nv.ptr(wp), nv.ptr(y), nv.dtype_code(dt), nv.dtype_code(ydt), n, s_in, s_in,
-                      layer.cin_p, layer.cout_p, layer.out_channels, k, k, pad, conv, conv, nv.ptr(os_), nv.ptr(bp), 0,
-                      0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(x), x.device)
+        _synth_conv_fwd(layer, a, os_, dt, y)
         del a
         out = layer.flrelu_nhwc(y, dt)
         ctx.save_for_backward(x, xs, os_, y)

@@ -479,6 +479,23 @@ class SynthesisLayer(torch.nn.Module):
         self._cache[("adj", dt)] = (key, wt)
         return wt
 
+    def packed_adjoint_wino(self):
+        """packed_adjoint for the Winograd kernel: U [cin_p][3][4][cout_p] f16 of the normalised W flipped in space
+        and transposed in channels (ic2_pack_weight_wino on the f32 adjoint, no further normalisation)."""
+        key = _version_key(self.weight)
+        hit = self._cache.get("adj_wino")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w = self.weight.detach().to(torch.float32)
+        if not self.is_torgb:
+            w = w * w.square().mean(dim=[1, 2, 3], keepdim=True).rsqrt()
+        wa = w.transpose(0, 1).flip(2, 3).contiguous()
+        u = torch.empty([self.cin_p, 3, 4, self.cout_p], dtype=torch.float16, device=w.device)
+        nv.call("ic2_pack_weight_wino", nv.ptr(wa), self.in_channels, self.out_channels, self.cin_p, self.cout_p, 0,
+                1.0, nv.ptr(u), nv.F16, nv.stream_of(wa))
+        self._cache["adj_wino"] = (key, u)
+        return u
+
     def modulation_train(self, w):
         """Differentiable (xscale [n][cin_p], oscale [n][cout_p]) f32 from w [n, w_dim]: the same math as
         ic2_modconv_prep (styles = affine(w); demodulated layers: s * rsqrt(mean s^2) over the whole batch,

@@ -100,3 +100,37 @@ def test_conv_wino_plan_names_a_tile(cuda):
     for s in (36, 52, 84, 148, 276):
         name = nv.wino_plan(32, s, s, 512, 512, 2)
         assert name.startswith("wino_fx_o128_p") and name.endswith("_f16"), name
+
+
+def test_wino_adjoint_dgrad_matches_fp64(cuda):
+    """The training path's dgrad through the Winograd kernel: conv_nhwc on the adjoint weights (normalised W flipped
+    in space, transposed in channels, packed by SynthesisLayer.packed_adjoint_wino) equals dL/da = conv_transpose2d
+    of the gradient with W_norm (pad 2 forward -> valid adjoint), next to the direct implicit GEMM on the same pack."""
+    from image_compression_2_amd import autograd_ops as ao
+    from image_compression_2_amd.networks_stylegan3 import SynthesisLayer
+
+    torch.manual_seed(0)
+    L = SynthesisLayer(w_dim=512, is_torgb=False, is_critically_sampled=False, use_fp16=False, in_channels=250,
+                       out_channels=320, in_size=50, out_size=50, in_sampling_rate=16, out_sampling_rate=16,
+                       in_cutoff=8, out_cutoff=8, in_half_width=4, out_half_width=4).to(cuda)
+    n, s_in = 2, 50
+    conv = s_in + 2
+    assert nv.wino_preferred(nv.F16, n, conv, conv, L.cout_p, L.cin_p, 3, 3, 0)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    dc = torch.zeros(n, conv, conv, L.cout_p, device=cuda, dtype=torch.float16)
+    dc[..., :L.out_channels] = torch.randn(n, conv, conv, L.out_channels, device=cuda, generator=g).to(torch.float16)
+    with torch.no_grad():
+        da_w = ao.conv_nhwc(dc, L.packed_adjoint(torch.float16), None, L.in_channels, 3, 0, wino=L.packed_adjoint_wino)
+        da_d = ao.conv_nhwc(dc, L.packed_adjoint(torch.float16), None, L.in_channels, 3, 0)
+    torch.cuda.synchronize()
+    w = L.weight.detach().double()
+    wn = w * w.square().mean([1, 2, 3], keepdim=True).rsqrt()
+    ref = F.conv_transpose2d(dc[..., :L.out_channels].double().permute(0, 3, 1, 2), wn, padding=2)
+    got_w = da_w[..., :L.in_channels].double().permute(0, 3, 1, 2)
+    got_d = da_d[..., :L.in_channels].double().permute(0, 3, 1, 2)
+    scale = ref.abs().max().item()
+    e_w, e_d = (got_w - ref).abs().max().item() / scale, (got_d - ref).abs().max().item() / scale
+    print(f"[adjoint wino] rel err wino {e_w:.2e}, direct {e_d:.2e}")
+    assert e_w < 4e-3 and e_w <= 4 * e_d + 1e-4, (e_w, e_d)
+    if L.cin_p > L.in_channels:  # padded input channels: zero adjoint rows
+        assert da_w[..., L.in_channels:].abs().max().item() == 0.0
