@@ -157,3 +157,106 @@ def allreduce_gradients(params, world=None, bucket_bytes=64 << 20):
             g.copy_(flat[off:off + k].view_as(g))
             off += k
     return len(buckets)
+
+
+class GradReducer:
+    """The gradient average of ``allreduce_gradients``, overlapped with backward: every parameter gets a
+    post-accumulate-grad hook; a bucket (parameters in reverse registration order -- the order backward produces
+    their gradients -- packed to about ``bucket_bytes``) is flattened and its all_reduce(SUM) launched
+    asynchronously (RCCL runs it on its own stream behind the flatten) as soon as its last gradient is accumulated,
+    while backward continues with the layers below.  Buckets launch strictly in index order (a completed bucket
+    waits for the ones before it), so every rank issues the same collective sequence.  ``finish()`` waits for the
+    handles, writes the averages back into .grad, and reduces what no hook covered: parameters created after the
+    reducer (the reference's per-call fc1, stylegan3_hvae_full.py:225-230) and buckets with a parameter that got no
+    gradient this step (the same on every rank: one module graph).
+
+    Usage per step: ``r.start(); loss.backward(); r.finish()``.  Autograd sums every use of a parameter before its
+    AccumulateGrad node runs, so a hook fires once per backward even with the training step's two encoder passes."""
+
+    def __init__(self, module, world=None, bucket_bytes=25 << 20):
+        self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        self.module = module
+        self.buckets = []
+        cur, size = [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * 4
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.slot = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self.slot[id(p)] = bi
+        self.active = False
+        self._handles = []
+        if self.world > 1:
+            for p in self.params:
+                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def start(self):
+        """Arm the hooks for one backward.  A parameter the module no longer holds (re-created since the reducer
+        was built) counts as ready, so its bucket does not wait for it."""
+        current = {id(p) for p in self.module.parameters()}
+        self.live = [[p for p in b if id(p) in current] for b in self.buckets]
+        self.ready = [len(b) - len(lv) for b, lv in zip(self.buckets, self.live)]
+        self.flat = [None] * len(self.buckets)
+        self.work = [None] * len(self.buckets)
+        self.next_launch = 0
+        self.active = self.world > 1
+        if self.active:
+            self._advance()
+
+    def _advance(self):
+        while self.next_launch < len(self.buckets) and self.ready[self.next_launch] == len(self.buckets[self.next_launch]):
+            self._launch(self.next_launch)
+            self.next_launch += 1
+
+    def _hook(self, p):
+        if not self.active:
+            return
+        bi = self.slot.get(id(p))
+        if bi is None:
+            return
+        self.ready[bi] += 1
+        self._advance()
+
+    def _launch(self, bi):
+        b = self.live[bi]
+        if not b:
+            return
+        flat = torch.cat([p.grad.reshape(-1).to(torch.float32) for p in b])
+        self.flat[bi] = flat
+        self.work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
+
+    def finish(self):
+        """-> number of collectives issued (bucketed + leftover)."""
+        if not self.active:
+            return 0
+        self.active = False
+        n = 0
+        for bi, b in enumerate(self.live):
+            if self.work[bi] is None:
+                continue
+            self.work[bi].wait()
+            flat = self.flat[bi].div_(self.world)
+            off = 0
+            for p in b:
+                k = p.numel()
+                p.grad.copy_(flat[off:off + k].view_as(p.grad))
+                off += k
+            n += 1
+        done = {id(p) for bi, b in enumerate(self.live) if self.work[bi] is not None for p in b}
+        rest = [p for p in self.module.parameters() if p.grad is not None and id(p) not in done]
+        n += allreduce_gradients(rest, self.world)
+        self.flat = [None] * len(self.buckets)
+        self.work = [None] * len(self.buckets)
+        return n

@@ -85,6 +85,20 @@ def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_
             proj.fc1_hook = None
 
 
+def _reducer(encoder, world):
+    """The encoder's overlapped gradient reducer (distributed.GradReducer, built on the first data-parallel step),
+    or None: single process, or IC2_OVERLAP_ALLREDUCE=0 (the post-backward allreduce_gradients, for A/B)."""
+    import os
+    if world is None:
+        world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if world <= 1 or os.environ.get("IC2_OVERLAP_ALLREDUCE", "1") == "0":
+        return None
+    r = getattr(encoder, "_grad_reducer", None)
+    if r is None or r.world != world:
+        r = encoder._grad_reducer = icd.GradReducer(encoder, world)
+    return r
+
+
 def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight, percep,
                 second_encoder_pass, sync_gradients, scaler=None):
     with torch.enable_grad(), ao.derived_cache():
@@ -101,9 +115,15 @@ def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perce
         perceptual = percep(images, reconstructed).mean() if percep is not None else rec_loss.new_zeros(())
         kl = kl_divergence(means, logvars, w_avg)
         loss = rec_weight * rec_loss + perceptual_weight * perceptual + kl_weight * kl
+        reducer = _reducer(encoder, sync_gradients)
+        if reducer is not None:
+            reducer.start()   # bucket all_reduces launched from backward as their gradients complete
         (scaler.scale(loss) if scaler is not None else loss).backward()
     # the average of scaled gradients is the scaled average: the scaler unscales after the all_reduce
-    icd.allreduce_gradients(list(encoder.parameters()), sync_gradients)
+    if reducer is not None:
+        reducer.finish()
+    else:
+        icd.allreduce_gradients(list(encoder.parameters()), sync_gradients)
     if scaler is not None:
         scaler.step(optimizer)
         scaler.update()

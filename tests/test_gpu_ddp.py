@@ -17,7 +17,8 @@ ENC64 = dict(img_resolution=64, img_channels=3, w_dim=512, num_ws=16, block_spli
              channel_max=64)
 
 
-def _ddp_worker(out, steps):
+def _ddp_worker(out, steps, overlap="1"):
+    os.environ["IC2_OVERLAP_ALLREDUCE"] = overlap
     import torch.distributed as dist
     import image_compression_2_amd as ic2
     from image_compression_2_amd import training as ict
@@ -59,3 +60,17 @@ def test_data_parallel_train_step_ranks_agree(cuda, tmp_path):
     assert r0["moved"] >= r0["n"] // 2 and r1["moved"] == r0["moved"]
     assert all(np.isfinite(r0["losses"])) and all(np.isfinite(r1["losses"]))
     assert r0["losses"][0] != r1["losses"][0]
+
+
+def test_overlapped_gradient_allreduce_matches_post_backward(cuda, tmp_path):
+    """distributed.GradReducer (bucket all_reduces launched from backward hooks, the default) and the post-backward
+    allreduce_gradients (IC2_OVERLAP_ALLREDUCE=0) give bit-identical weights after two steps: a two-rank sum does
+    not depend on the bucketing or the order, and the ranks run the same seeded step either way."""
+    a, b = str(tmp_path / "ov"), str(tmp_path / "pb")
+    icd.launch(2, _ddp_worker, a, 2, "1")
+    icd.launch(2, _ddp_worker, b, 2, "0")
+    for r in range(2):
+        pa, pb = (torch.load(f"{o}.{r}", weights_only=True) for o in (a, b))
+        diff = [k for k in pa["params"] if not torch.equal(pa["params"][k], pb["params"][k])]
+        assert not diff, diff[:5]
+        assert pa["losses"] == pb["losses"]

@@ -193,3 +193,76 @@ def test_derived_cache_scope():
         assert len(calls) == 6
     ao._derived(p, ("k",), make)
     assert len(calls) == 7                      # the block's entries are gone
+
+
+class _ToyEncoder(torch.nn.Module):
+    """A parameter used twice per step (as the training step's two encoder passes use every weight), one that gets
+    no gradient, and a head re-created on every forward (the reference's fc1 quirk)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(6, 6)
+        self.b = torch.nn.Linear(6, 4)
+        self.unused = torch.nn.Parameter(torch.zeros(3))
+        self.head = torch.nn.Linear(4, 2)
+
+    def forward(self, x):
+        self.head = torch.nn.Linear(4, 2)   # fresh every call, like refresh_fc1
+        with torch.no_grad():
+            self.head.weight.fill_(0.5)
+            self.head.bias.fill_(0.1)
+        return self.head(torch.tanh(self.b(self.a(self.a(x)))))
+
+
+def _reducer_worker(out_path):
+    import torch.distributed as dist
+    rank, world, _ = icd.init("gloo")
+    torch.manual_seed(0)   # same weights on every rank
+    m = _ToyEncoder()
+    r = icd.GradReducer(m, world, bucket_bytes=64)   # several buckets
+    res = {}
+    for step in range(2):
+        x = torch.randn(5, 6, generator=torch.Generator().manual_seed(10 * step + rank))   # this rank's slice
+        m.zero_grad(set_to_none=True)
+        loss = m(x).square().sum() + m(x).sum()   # two passes, as the training step
+        r.start()
+        loss.backward()
+        launched = r.next_launch
+        n = r.finish()
+        got = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        # the same gradients reduced after backward
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(0)
+        loss = m(x).square().sum() + m(x).sum()
+        loss.backward()
+        icd.allreduce_gradients(list(m.parameters()), world)
+        ref = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        res[step] = {"got": got, "ref": ref, "launched": launched, "n": n, "unused": m.unused.grad is None}
+    torch.save(res, f"{out_path}.{rank}")
+    r.remove()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_overlapped_matches_post_backward_allreduce(tmp_path):
+    out = str(tmp_path / "gr")
+    icd.launch(2, _reducer_worker, out)
+    res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    for step in range(2):
+        for rk in range(2):
+            d = res[rk][step]
+            assert set(d["got"]) == set(d["ref"]) == {"a.weight", "a.bias", "b.weight", "b.bias", "head.weight",
+                                                      "head.bias"}
+            for k in d["ref"]:
+                assert torch.allclose(d["got"][k], d["ref"][k], atol=1e-6), (step, k)
+                assert torch.allclose(d["got"][k], res[0][step]["got"][k]), "ranks disagree"
+            assert d["launched"] >= 1, "no bucket launched during backward"
+            assert d["unused"]
+
+
+def test_grad_reducer_single_process_is_inert():
+    m = _ToyEncoder()
+    r = icd.GradReducer(m, world=1)
+    r.start()
+    m(torch.randn(2, 6)).sum().backward()
+    assert r.finish() == 0 and not r._handles
