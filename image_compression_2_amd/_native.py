@@ -88,6 +88,7 @@ _SIGS = {
     "ic2_flrelu_bwd_nhwc_ex": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                                _F, _F, _F, _I, _P, _P, _P, _I64, _P],
     "ic2_scale_bwd_part_floats": [_I, _I, _I],
+    "ic2_colsum_div": [_P, _I, _I, _I, _P, _P, _P],
     "ic2_scale_bwd_nhwc": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I64, _P],
     "ic2_scale_nhwc": [_P, _P, _P, _I, _I, _I, _I, _P],
     "ic2_conv3x3_gn_stats_floats": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
@@ -322,3 +323,15 @@ def pad_synth(c):
     channel).  The SG3-T-256 strides (181 -> 192, 362 -> 384) are unchanged."""
     c = int(c)
     return pad32(c) if c <= 128 else (c + 63) // 64 * 64
+
+
+def colsum_div(part, n, c, den=None):
+    """out [n, c] f32 = part.view(n, -1, c).sum(1) / den (0 where den == 0; den None: the plain sum), one launch
+    (ic2_colsum_div)."""
+    part = part.contiguous()
+    rows = part.numel() // (n * c)
+    assert rows * n * c == part.numel(), (part.shape, n, c)
+    out = torch.empty([n, c], dtype=torch.float32, device=part.device)
+    call("ic2_colsum_div", ptr(part), n, rows, c, None if den is None else ptr(den.contiguous()), ptr(out),
+         stream_of(part))
+    return out

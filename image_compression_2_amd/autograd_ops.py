@@ -266,13 +266,13 @@ def _synth_layer_grads(L, dt, os_, y, dout):
             py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(os_), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
         if rc not in (0, 2):
             raise RuntimeError(f"ic2_flrelu_bwd_nhwc_ex failed: {nv.load().ic2_last_error().decode()}")
-    if rc == 0:
-        yd = ydot.view(n, -1, c_p).sum(1)
+    if rc == 0:   # dL/doscale = sum over tiles of the ydot partials / oscale (0 where oscale is 0), one launch
+        d_os = nv.colsum_div(ydot, n, c_p, os_.detach().float())
     else:   # no fused instance for this geometry: the composed HIP path + torch epilogue
         gy = _flrelu_backward_composed(y, dout, L)
         dc.copy_(gy * os_[:, None, None, :])
         yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
-    d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
+        d_os = torch.where(os_ != 0, yd / torch.where(os_ != 0, os_, torch.ones_like(os_)), torch.zeros_like(os_))
     # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1)
     da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0,
                    wino=L.packed_adjoint_wino if dt == torch.float16 else None)
@@ -334,8 +334,7 @@ class SynthLayerScaledNHWC(torch.autograd.Function):
         dout = torch.empty_like(out)
         nv.call("ic2_scale_bwd_nhwc", nv.ptr(g), nv.ptr(out), nv.ptr(xs), nv.ptr(dout), nv.dtype_code(out.dtype), n,
                 ho * wo, c_p, nv.ptr(part), npart, nv.stream_of(out))
-        s = part.view(n, -1, c_p).sum(1)
-        d_xs = torch.where(xs != 0, s / torch.where(xs != 0, xs, torch.ones_like(xs)), torch.zeros_like(xs))
+        d_xs = nv.colsum_div(part, n, c_p, xs)   # sum_p g * out / xs_next, 0 where xs_next = 0
         da, d_os = _synth_layer_grads(L, dt, os_, y, dout)
         return da, d_os, d_xs, None, None
 
@@ -366,7 +365,7 @@ class ScaleNHWC(torch.autograd.Function):
         dx = torch.empty_like(x)
         nv.call("ic2_scale_bwd_nhwc", nv.ptr(da), nv.ptr(x), nv.ptr(xs), nv.ptr(dx), nv.dtype_code(x.dtype), n, h * w,
                 c_p, nv.ptr(part), npart, nv.stream_of(x))
-        return dx, part.view(n, -1, c_p).sum(1)
+        return dx, nv.colsum_div(part, n, c_p)
 
 
 class FrozenConvNHWC(torch.autograd.Function):
@@ -495,5 +494,5 @@ class SynthLayerNHWC(torch.autograd.Function):
         dx = torch.empty_like(x)
         nv.call("ic2_scale_bwd_nhwc", nv.ptr(da), nv.ptr(x), nv.ptr(xs), nv.ptr(dx), nv.dtype_code(x.dtype), n, hi * wi,
                 cin_p, nv.ptr(part), npart, nv.stream_of(y))
-        d_xs = part.view(n, -1, cin_p).sum(1)
+        d_xs = nv.colsum_div(part, n, cin_p)
         return dx, d_xs, d_os, None, None

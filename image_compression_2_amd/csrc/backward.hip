@@ -733,6 +733,32 @@ extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xs
   return IC2_OK;
 }
 
+// out[n][c] = (sum over r of part[n][r][c]) / den[n][c], 0 where den[n][c] == 0 (no den: the plain sum).  One thread
+// per (n, c), rows summed in order: deterministic.
+__global__ void __launch_bounds__(256) colsum_div_kernel(const float* __restrict__ part, int rows, int c, int nc,
+                                                         const float* __restrict__ den, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc) return;
+  const int nn = i / c, ch = i - nn * c;
+  const float* p = part + (int64_t)nn * rows * c + ch;
+  float t = 0.f;
+  for (int r = 0; r < rows; ++r) t += p[(int64_t)r * c];
+  if (den != nullptr) {
+    const float d = den[i];
+    t = d != 0.f ? t / d : 0.f;
+  }
+  out[i] = t;
+}
+
+extern "C" int ic2_colsum_div(const float* part, int n, int rows, int c, const float* den, float* out, void* stream) {
+  IC2_CHECK_ARG(part && out && n > 0 && rows > 0 && c > 0 && (int64_t)n * c < (1LL << 31), "colsum_div: bad arguments");
+  const int nc = n * c;
+  hipLaunchKernelGGL(colsum_div_kernel, dim3((unsigned)ceil_div(nc, 256)), dim3(256), 0, as_stream(stream), part, rows,
+                     c, nc, den, out);
+  IC2_CHECK_LAUNCH("colsum_div");
+  return IC2_OK;
+}
+
 extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad) {
   WgradArgs a{};
   a.ho = h + 2 * pad - kh + 1;

@@ -395,6 +395,13 @@ int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p);
 int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw, int c_p,
                        float* part, int64_t part_floats, void* stream);
 
+/* The per-(sample, channel) finish of those partial sums: out[n][c] = (sum over r of part[n][r][c]) / den[n][c], and 0
+ * where den[n][c] == 0 (den = NULL: the plain sum).  part [n][rows][c] f32 (ic2_scale_bwd_nhwc's part, or
+ * ic2_flrelu_bwd_nhwc_ex's ydot), out [n][c] f32.  dL/dxscale = sum / xscale_next on the modulation-folded path and
+ * dL/doscale = sum / oscale: the torch `where(den != 0, sum / den, 0)` chain of SG3's modulated_conv2d backward
+ * (stylegan3_hvae_full.py:274) in one launch.  Deterministic (rows summed in order). */
+int ic2_colsum_div(const float* part, int n, int rows, int c, const float* den, float* out, void* stream);
+
 /* Its forward on the training path (SynthLayerNHWC; inference folds xscale into the producer's epilogue):
  * a[n][p][c] = x[n][p][c] * xscale[n][c], NHWC f32 / bf16, c_p % 8 == 0.  Replaces the reference's
  * `x * styles` broadcast inside modulated_conv2d (SG3-public, called at stylegan3_hvae_full.py:274). */

@@ -662,3 +662,20 @@ def test_f16_train_step_graph_capture_replays_sane_losses(cuda):
         assert 0.5 * ref < rec < 2.0 * ref, (rec, eager)
     assert any(not torch.equal(a, b.detach()) for a, b in zip(before, enc.parameters()))
     assert all(torch.isfinite(p).all() for p in enc.parameters())
+
+
+def test_colsum_div_matches_torch_where_chain(cuda):
+    """ic2_colsum_div (the d oscale / d xscale finish of the synthesis backward) equals the torch chain it replaced,
+    where(den != 0, part.view(n, -1, c).sum(1) / den, 0), including zero denominators, and the plain column sum."""
+    from image_compression_2_amd import _native as nv
+    g = torch.Generator(device=cuda).manual_seed(0)
+    for n, rows, c in ((3, 17, 96), (16, 256, 512), (1, 1, 32)):
+        part = torch.randn(n, rows, c, device=cuda, generator=g)
+        den = torch.randn(n, c, device=cuda, generator=g)
+        den[:, ::7] = 0.0
+        got = nv.colsum_div(part, n, c, den)
+        s = part.double().sum(1)
+        ref = torch.where(den != 0, s / torch.where(den != 0, den.double(), torch.ones_like(s)), torch.zeros_like(s))
+        assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+        assert (got[:, ::7] == 0).all()
+        assert torch.allclose(nv.colsum_div(part, n, c).double(), s, rtol=1e-5, atol=1e-4)

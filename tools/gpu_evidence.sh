@@ -22,7 +22,7 @@ for p in $parts; do
     c5) run c5 --config c5 --steps 20 --warmup 5 --cpu-baseline-images 0 ;;
     trace)
       for cfg in c2 c4; do
-        timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $o/prof_$cfg -o run -- python3 bench.py --config $cfg \
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $o/prof_$cfg -o run -- python3 bench.py --config $cfg --no-secondary \
           --steps 20 --warmup 3 --cpu-baseline-images 0 --no-roofline --no-parity > $o/${tag}_prof_$cfg.log 2>&1 \
           || { tail -20 $o/${tag}_prof_$cfg.log; exit 1; }
         tr=$(find $o/prof_$cfg -name "*kernel_trace.csv" | head -1)
