@@ -83,6 +83,8 @@ _SIGS = {
     "ic2_gn_lrelu_pool_bwd_floats": [_I, _I, _I, _I, _I],
     "ic2_gn_lrelu_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _I64,
                               _P],
+    "ic2_gn_lrelu_pool_bwd_db": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P,
+                                 _I64, _P],
     "ic2_gap_bwd": [_P, _P, _I, _I, _I, _I, _I, _P],
     "ic2_flrelu_bwd_ydot_floats": [_I, _I, _I, _I, _I],
     "ic2_flrelu_bwd_nhwc_ex": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,

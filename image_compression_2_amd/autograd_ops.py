@@ -141,6 +141,9 @@ class Conv2dNHWC(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         cout, cin, kh, kw = weight.shape
         n, h, w, cin_p = x.shape
+        colsum = getattr(dy, "_ic2_colsum", None)   # from the GroupNorm backward that produced dy, if unchanged
+        if colsum is not None and (colsum[1] != dy._version or colsum[0].numel() < cout):
+            colsum = None
         dy = dy.to(x.dtype).contiguous()
         cout_p = dy.shape[-1]
         dx = dw = db = None
@@ -157,8 +160,10 @@ class Conv2dNHWC(torch.autograd.Function):
                     cout_p, kh, kw, ctx.pad, nv.ptr(ws), nfl, nv.stream_of(x))
             dw = dwp[:cout, :, :, :cin].permute(0, 3, 1, 2).contiguous()
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            # f32 accumulation straight from the 16-bit gradient (no f32 copy of dy)
-            db = dy.reshape(-1, cout_p).sum(0, dtype=torch.float32)[:cout]
+            if colsum is not None:   # the GroupNorm backward's f64 channel sums: no pass over dy
+                db = colsum[0][:cout]
+            else:   # f32 accumulation straight from the 16-bit gradient (no f32 copy of dy)
+                db = dy.reshape(-1, cout_p).sum(0, dtype=torch.float32)[:cout]
         return dx, dw, db, None, None
 
 
@@ -193,10 +198,14 @@ class GroupNormLReluPoolNHWC(torch.autograd.Function):
         dy = torch.empty_like(y)
         dgamma = torch.empty([c], dtype=torch.float32, device=y.device)
         dbeta = torch.empty([c], dtype=torch.float32, device=y.device)
-        nv.call("ic2_gn_lrelu_pool_bwd", nv.ptr(y), nv.ptr(dout), nv.ptr(dy), nv.dtype_code(y.dtype),
+        dsum = torch.empty([c], dtype=torch.float32, device=y.device)
+        nv.call("ic2_gn_lrelu_pool_bwd_db", nv.ptr(y), nv.ptr(dout), nv.ptr(dy), nv.dtype_code(y.dtype),
                 nv.dtype_code(dout.dtype), nv.dtype_code(dy.dtype), n, h, w, c_p, c, groups, nv.ptr(stats),
-                nv.ptr(g32), nv.ptr(b32), float(slope), int(pool), nv.ptr(dgamma), nv.ptr(dbeta), nv.ptr(ws), nfl,
-                nv.stream_of(y))
+                nv.ptr(g32), nv.ptr(b32), float(slope), int(pool), nv.ptr(dgamma), nv.ptr(dbeta), nv.ptr(dsum),
+                nv.ptr(ws), nfl, nv.stream_of(y))
+        # sum of dy over (n, p): the producing conv's bias gradient (Conv2dNHWC.backward reads it instead of
+        # reducing dy again); stamped with dy's version so an in-place accumulation into dy invalidates it
+        dy._ic2_colsum = (dsum, dy._version)
         return dy, dgamma, dbeta, None, None, None, None, None, None
 
 

@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float slope, int pool,
                                                           int nchunks, float* __restrict__ part) {
-  __shared__ float sAB[256 * 17];  // [thread][8 A, 8 B] (+1: odd row pitch)
+  __shared__ float sAB[256 * 25];  // [thread][8 A, 8 B, 8 X] (+1: odd row pitch)
   const int hw = h * w;
   const int chunk = blockIdx.x % nchunks, nn = blockIdx.x / nchunks;
   const int p0 = chunk * GNB_CHUNK, p1 = min(hw, p0 + GNB_CHUNK);
@@ -425,9 +425,9 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__
   const int cl = threadIdx.x % CT, ph = threadIdx.x / CT;
   for (int cb = 0; cb < C8; cb += CT) {
     const int c8 = cb + cl, cc0 = 8 * c8;
-    float sa[8], sb[8];
+    float sa[8], sb[8], sx[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
+    for (int j = 0; j < 8; ++j) sa[j] = sb[j] = sx[j] = 0.f;
     if (ph < PS && c8 < C8 && cc0 < c) {
       float mean[8], rstd[8], gam[8], bet[8], valid[8];
 #pragma unroll
@@ -452,72 +452,94 @@ __global__ void __launch_bounds__(256) gnb_partial_kernel(const TY* __restrict__
           const float dz = gnb_dz(yv[j], dv[j] * valid[j], mean[j], rstd[j], gam[j], bet[j], slope, xhat);
           sa[j] += dz;
           sb[j] += dz * xhat;
+          sx[j] += xhat;
         }
       }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sAB[threadIdx.x * 17 + j] = sa[j];
-      sAB[threadIdx.x * 17 + 8 + j] = sb[j];
+      sAB[threadIdx.x * 25 + j] = sa[j];
+      sAB[threadIdx.x * 25 + 8 + j] = sb[j];
+      sAB[threadIdx.x * 25 + 16 + j] = sx[j];
     }
     __syncthreads();
     if (ph == 0 && c8 < C8) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float a = 0.f, b = 0.f;
+        float a = 0.f, b = 0.f, x = 0.f;
         for (int k = 0; k < PS; ++k) {
-          a += sAB[(k * CT + cl) * 17 + j];
-          b += sAB[(k * CT + cl) * 17 + 8 + j];
+          a += sAB[(k * CT + cl) * 25 + j];
+          b += sAB[(k * CT + cl) * 25 + 8 + j];
+          x += sAB[(k * CT + cl) * 25 + 16 + j];
         }
-        float* o = part + (((int64_t)nn * c_p + cc0 + j) * nchunks + chunk) * 2;
+        float* o = part + (((int64_t)nn * c_p + cc0 + j) * nchunks + chunk) * 3;
         o[0] = a;
         o[1] = b;
+        o[2] = x;
       }
     }
   }
 }
 
-// per (n, c): ordered f64 sum over the chunks -> AB[n][c][2]
+// per (n, c): ordered f64 sum over the chunks -> AB[n][c][3] (sum dz, sum dz * xhat, sum xhat)
 __global__ void __launch_bounds__(256) gnb_chunks_kernel(const float* __restrict__ part, int nc, int nchunks,
                                                          double* __restrict__ ab) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= nc) return;
-  double a = 0.0, b = 0.0;
+  double a = 0.0, b = 0.0, x = 0.0;
   for (int k = 0; k < nchunks; ++k) {
-    a += part[((int64_t)i * nchunks + k) * 2];
-    b += part[((int64_t)i * nchunks + k) * 2 + 1];
+    a += part[((int64_t)i * nchunks + k) * 3];
+    b += part[((int64_t)i * nchunks + k) * 3 + 1];
+    x += part[((int64_t)i * nchunks + k) * 3 + 2];
   }
-  ab[2 * i] = a;
-  ab[2 * i + 1] = b;
+  ab[3 * i] = a;
+  ab[3 * i + 1] = b;
+  ab[3 * i + 2] = x;
 }
 
 // one thread per (n, g): S1, S2 (f32 out, divided by Ng); then one thread per channel: dbeta, dgamma (sum over n)
+// and, when asked, the sum of dy over (n, p) -- the bias gradient of the conv that produced y:
+//   sum_p dy = rstd * (gamma * sum_p dz - HW * S1 / Ng - (S2 / Ng) * sum_p xhat)   per (n, c), in f64
 __global__ void __launch_bounds__(256) gnb_group_kernel(const double* __restrict__ ab, int n, int c_p, int c,
                                                         int groups, double ng, const float* __restrict__ gamma,
+                                                        const float* __restrict__ stats, double hw,
                                                         float* __restrict__ s12, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta) {
+                                                        float* __restrict__ dbeta, float* __restrict__ dsum) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int cpg = c / groups;
-  if (i < n * groups) {
-    const int nn = i / groups, gi = i - (i / groups) * groups;
-    double s1 = 0.0, s2 = 0.0;
+  auto group_s = [&](int nn, int gi, double& s1, double& s2) {
+    s1 = s2 = 0.0;
     for (int k = 0; k < cpg; ++k) {
       const int cc = gi * cpg + k;
-      s1 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 2];
-      s2 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 2 + 1];
+      s1 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 3];
+      s2 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 3 + 1];
     }
+  };
+  if (i < n * groups) {
+    const int nn = i / groups, gi = i - (i / groups) * groups;
+    double s1, s2;
+    group_s(nn, gi, s1, s2);
     s12[2 * i] = (float)(s1 / ng);
     s12[2 * i + 1] = (float)(s2 / ng);
   }
   if (i < c) {
-    double db = 0.0, dg = 0.0;
+    double db = 0.0, dg = 0.0, ds = 0.0;
+    const int gi = i / cpg;
     for (int nn = 0; nn < n; ++nn) {
-      db += ab[((int64_t)nn * c_p + i) * 2];
-      dg += ab[((int64_t)nn * c_p + i) * 2 + 1];
+      const double a = ab[((int64_t)nn * c_p + i) * 3], b = ab[((int64_t)nn * c_p + i) * 3 + 1];
+      db += a;
+      dg += b;
+      if (dsum) {
+        double s1, s2;
+        group_s(nn, gi, s1, s2);
+        const double rstd = (double)stats[(nn * groups + gi) * 2 + 1];
+        ds += rstd * ((double)gamma[i] * a - hw * (s1 / ng) - (s2 / ng) * ab[((int64_t)nn * c_p + i) * 3 + 2]);
+      }
     }
     if (dbeta) dbeta[i] = (float)db;
     if (dgamma) dgamma[i] = (float)dg;
+    if (dsum) dsum[i] = (float)ds;
   }
 }
 
@@ -827,14 +849,29 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
 
 extern "C" int64_t ic2_gn_lrelu_pool_bwd_floats(int n, int h, int w, int c_p, int groups) {
   const int64_t nchunks = ceil_div((int64_t)h * w, GNB_CHUNK);
-  // part [n][c_p][nchunks][2] f32 | ab [n][c_p][2] f64 | s12 [n][groups][2] f32
-  return (int64_t)n * c_p * nchunks * 2 + (int64_t)n * c_p * 2 * 2 + (int64_t)n * groups * 2 + 4;
+  // part [n][c_p][nchunks][3] f32 | ab [n][c_p][3] f64 | s12 [n][groups][2] f32
+  return (int64_t)n * c_p * nchunks * 3 + (int64_t)n * c_p * 3 * 2 + (int64_t)n * groups * 2 + 4;
 }
+
+extern "C" int ic2_gn_lrelu_pool_bwd_db(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout,
+                                        int dtype_dy, int n, int h, int w, int c_p, int c, int groups,
+                                        const float* stats, const float* gamma, const float* beta, float slope,
+                                        int pool, float* dgamma, float* dbeta, float* dsum, float* workspace,
+                                        int64_t ws_floats, void* stream);
 
 extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout,
                                      int dtype_dy, int n, int h, int w, int c_p, int c, int groups, const float* stats,
                                      const float* gamma, const float* beta, float slope, int pool, float* dgamma,
                                      float* dbeta, float* workspace, int64_t ws_floats, void* stream) {
+  return ic2_gn_lrelu_pool_bwd_db(y, dout, dy, dtype_y, dtype_dout, dtype_dy, n, h, w, c_p, c, groups, stats, gamma,
+                                  beta, slope, pool, dgamma, dbeta, nullptr, workspace, ws_floats, stream);
+}
+
+extern "C" int ic2_gn_lrelu_pool_bwd_db(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout,
+                                        int dtype_dy, int n, int h, int w, int c_p, int c, int groups,
+                                        const float* stats, const float* gamma, const float* beta, float slope,
+                                        int pool, float* dgamma, float* dbeta, float* dsum, float* workspace,
+                                        int64_t ws_floats, void* stream) {
   IC2_CHECK_ARG(y && dout && dy && stats && gamma && beta && workspace && n > 0 && h > 0 && w > 0 && c > 0 &&
                     c <= c_p && groups > 0 && c % groups == 0,
                 "gn_lrelu_pool_bwd: bad arguments");
@@ -848,8 +885,8 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
                 "gn_lrelu_pool_bwd: bad dtypes (f16 only as f16 y, dout and dy)");
   const int nchunks = (int)ceil_div((int64_t)h * w, GNB_CHUNK);
   float* part = workspace;
-  double* ab = reinterpret_cast<double*>(workspace + (((int64_t)n * c_p * nchunks * 2 + 1) / 2) * 2);
-  float* s12 = reinterpret_cast<float*>(ab + (int64_t)n * c_p * 2);
+  double* ab = reinterpret_cast<double*>(workspace + (((int64_t)n * c_p * nchunks * 3 + 1) / 2) * 2);
+  float* s12 = reinterpret_cast<float*>(ab + (int64_t)n * c_p * 3);
   hipStream_t s = as_stream(stream);
   const double ng = (double)h * w * (c / groups);
   // pass 4: (pixel blocks, n); a block covers 256 / min(c_p / 8, 256) pixels per step, ~4 steps per thread
@@ -865,7 +902,7 @@ extern "C" int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, 
                        nchunks, ab);                                                                             \
     const int ng_th = n * groups > c ? n * groups : c;                                                           \
     hipLaunchKernelGGL(gnb_group_kernel, dim3((unsigned)ceil_div(ng_th, 256)), dim3(256), 0, s, ab, n, c_p, c,     \
-                       groups, ng, gamma, s12, dgamma, dbeta);                                                   \
+                       groups, ng, gamma, stats, (double)h * w, s12, dgamma, dbeta, dsum);                       \
     if (dtype_dy == IC2_F32)                                                                                     \
       hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, float>), apply_grid, dim3(256), 0, s, (const TY*)y,             \
                          (const TD*)dout, (float*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,    \

@@ -327,6 +327,13 @@ int ic2_gn_lrelu_pool_bwd(const void* y, const void* dout, void* dy, int dtype_y
                           int h, int w, int c_p, int c, int groups, const float* stats, const float* gamma,
                           const float* beta, float slope, int pool, float* dgamma, float* dbeta, float* workspace,
                           int64_t ws_floats, void* stream);
+/* The same, plus dsum[c] = sum over (n, p) of dy (nullable): the bias gradient of the conv whose output y is
+ * (VGGBlock :183-191, conv -> GroupNorm), from the pass-1 channel sums (sum dz, sum dz * xhat, sum xhat) in f64
+ * instead of a reduction over the stored dy. */
+int ic2_gn_lrelu_pool_bwd_db(const void* y, const void* dout, void* dy, int dtype_y, int dtype_dout, int dtype_dy,
+                             int n, int h, int w, int c_p, int c, int groups, const float* stats, const float* gamma,
+                             const float* beta, float slope, int pool, float* dgamma, float* dbeta, float* dsum,
+                             float* workspace, int64_t ws_floats, void* stream);
 
 /* Backward of ic2_global_avg_pool (AdaptiveAvgPool2d(1), :218): dx [n][hw][c_p] = dpooled [n][c] / hw. */
 int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_p, int c, void* stream);

@@ -156,6 +156,26 @@ def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
     tol = {torch.float32: 1e-4, torch.bfloat16: 3e-2, torch.float16: 4e-3}[dtype]
     assert _rel(yd.grad.float().cpu()[..., :c].permute(0, 3, 1, 2), yr.grad) < tol
     assert _rel(gd.grad, gr.grad) < tol and _rel(bd.grad, br.grad) < tol
+    # the producing conv's bias gradient from the same call (ic2_gn_lrelu_pool_bwd_db's dsum, f64 channel sums):
+    # sum over (n, p) of dy, against the fp64 reference and the column sum of the dy it stored
+    yn = ao.ToNHWC.apply(y.to(cuda), dtype, c_p).contiguous()
+    nfl = int(nv.query("ic2_group_norm_stats_floats", n, h * w, groups))
+    stats = torch.empty([nfl], dtype=torch.float32, device=cuda)
+    st = nv.stream_of(yn)
+    nv.call("ic2_group_norm_stats", nv.ptr(yn), nv.dtype_code(dtype), n, h * w, c_p, c, groups, 1e-5, nv.ptr(stats),
+            st)
+    dn = F.pad(dout, (0, c_p - c)).to(cuda, dtype).contiguous()
+    wsf = int(nv.query("ic2_gn_lrelu_pool_bwd_floats", n, h, w, c_p, groups))
+    ws = torch.empty([wsf], dtype=torch.float32, device=cuda)
+    dy = torch.empty_like(yn)
+    dsum = torch.empty([c], dtype=torch.float32, device=cuda)
+    g32, b32 = gam.to(cuda), bet.to(cuda)
+    nv.call("ic2_gn_lrelu_pool_bwd_db", nv.ptr(yn), nv.ptr(dn), nv.ptr(dy), nv.dtype_code(dtype), nv.dtype_code(dtype),
+            nv.dtype_code(dtype), n, h, w, c_p, c, groups, nv.ptr(stats), nv.ptr(g32), nv.ptr(b32), 0.2, int(pool), None,
+            None, nv.ptr(dsum), nv.ptr(ws), wsf, st)
+    ref_sum = yr.grad.sum(dim=(0, 2, 3))
+    assert _rel(dsum, ref_sum) < tol, (_rel(dsum, ref_sum), dtype)
+    assert _rel(dsum, dy.float()[..., :c].sum(dim=(0, 1, 2)).double()) < tol
 
 
 # ================================================================ synthesis backward (the frozen generator)
