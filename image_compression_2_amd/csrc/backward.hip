@@ -499,48 +499,53 @@ __global__ void __launch_bounds__(256) gnb_chunks_kernel(const float* __restrict
 }
 
 // one thread per (n, g): S1, S2 (f32 out, divided by Ng); then one thread per channel: dbeta, dgamma (sum over n)
-// and, when asked, the sum of dy over (n, p) -- the bias gradient of the conv that produced y:
-//   sum_p dy = rstd * (gamma * sum_p dz - HW * S1 / Ng - (S2 / Ng) * sum_p xhat)   per (n, c), in f64
 __global__ void __launch_bounds__(256) gnb_group_kernel(const double* __restrict__ ab, int n, int c_p, int c,
                                                         int groups, double ng, const float* __restrict__ gamma,
-                                                        const float* __restrict__ stats, double hw,
                                                         float* __restrict__ s12, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta, float* __restrict__ dsum) {
+                                                        float* __restrict__ dbeta) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int cpg = c / groups;
-  auto group_s = [&](int nn, int gi, double& s1, double& s2) {
-    s1 = s2 = 0.0;
+  if (i < n * groups) {
+    const int nn = i / groups, gi = i - (i / groups) * groups;
+    double s1 = 0.0, s2 = 0.0;
     for (int k = 0; k < cpg; ++k) {
       const int cc = gi * cpg + k;
       s1 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 3];
       s2 += (double)gamma[cc] * ab[((int64_t)nn * c_p + cc) * 3 + 1];
     }
-  };
-  if (i < n * groups) {
-    const int nn = i / groups, gi = i - (i / groups) * groups;
-    double s1, s2;
-    group_s(nn, gi, s1, s2);
     s12[2 * i] = (float)(s1 / ng);
     s12[2 * i + 1] = (float)(s2 / ng);
   }
   if (i < c) {
-    double db = 0.0, dg = 0.0, ds = 0.0;
-    const int gi = i / cpg;
+    double db = 0.0, dg = 0.0;
     for (int nn = 0; nn < n; ++nn) {
-      const double a = ab[((int64_t)nn * c_p + i) * 3], b = ab[((int64_t)nn * c_p + i) * 3 + 1];
-      db += a;
-      dg += b;
-      if (dsum) {
-        double s1, s2;
-        group_s(nn, gi, s1, s2);
-        const double rstd = (double)stats[(nn * groups + gi) * 2 + 1];
-        ds += rstd * ((double)gamma[i] * a - hw * (s1 / ng) - (s2 / ng) * ab[((int64_t)nn * c_p + i) * 3 + 2]);
-      }
+      db += ab[((int64_t)nn * c_p + i) * 3];
+      dg += ab[((int64_t)nn * c_p + i) * 3 + 1];
     }
     if (dbeta) dbeta[i] = (float)db;
     if (dgamma) dgamma[i] = (float)dg;
-    if (dsum) dsum[i] = (float)ds;
   }
+}
+
+// one thread per channel: the sum of dy over (n, p) -- the bias gradient of the conv that produced y -- from the
+// pass-1 channel sums and the same f32 S1 / Ng, S2 / Ng the apply pass uses:
+//   sum_p dy[n][p][c] = rstd * (gamma * sum_p dz - HW * s1 - s2 * sum_p xhat)
+__global__ void __launch_bounds__(256) gnb_dsum_kernel(const double* __restrict__ ab, int n, int c_p, int c, int groups,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ stats,
+                                                       const float* __restrict__ s12, double hw,
+                                                       float* __restrict__ dsum) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= c) return;
+  const int gi = i / (c / groups);
+  double ds = 0.0;
+  for (int nn = 0; nn < n; ++nn) {
+    const int sidx = nn * groups + gi;
+    const double* a = ab + ((int64_t)nn * c_p + i) * 3;
+    ds += (double)stats[2 * sidx + 1] *
+          ((double)gamma[i] * a[0] - hw * (double)s12[2 * sidx] - (double)s12[2 * sidx + 1] * a[2]);
+  }
+  dsum[i] = (float)ds;
 }
 
 // Pass 4: grid (pixel blocks, n); thread = 8 channels (fixed, coefficients in registers) x pixel lane
@@ -755,28 +760,47 @@ extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xs
   return IC2_OK;
 }
 
-// out[n][c] = (sum over r of part[n][r][c]) / den[n][c], 0 where den[n][c] == 0 (no den: the plain sum).  One thread
-// per (n, c), rows summed in order: deterministic.
-__global__ void __launch_bounds__(256) colsum_div_kernel(const float* __restrict__ part, int rows, int c, int nc,
+// out[n][c] = (sum over r of part[n][r][c]) / den[n][c], 0 where den[n][c] == 0 (no den: the plain sum).  Block =
+// (64 channels, sample): lane group k sums rows k, k+4, ... (coalesced 256-B rows, 4 loads in flight), the 4 group
+// sums combine in a fixed order through LDS: deterministic.
+__global__ void __launch_bounds__(256) colsum_div_kernel(const float* __restrict__ part, int rows, int c,
                                                          const float* __restrict__ den, float* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nc) return;
-  const int nn = i / c, ch = i - nn * c;
-  const float* p = part + (int64_t)nn * rows * c + ch;
+  __shared__ float red[4][64];
+  const int nn = blockIdx.y, cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cl;
   float t = 0.f;
-  for (int r = 0; r < rows; ++r) t += p[(int64_t)r * c];
-  if (den != nullptr) {
-    const float d = den[i];
-    t = d != 0.f ? t / d : 0.f;
+  if (ch < c) {
+    const float* p = part + (int64_t)nn * rows * c + ch;
+    int r = rg;
+    for (; r + 12 < rows; r += 16) {
+      const float a0 = p[(int64_t)r * c], a1 = p[(int64_t)(r + 4) * c], a2 = p[(int64_t)(r + 8) * c],
+                  a3 = p[(int64_t)(r + 12) * c];
+      t += a0;
+      t += a1;
+      t += a2;
+      t += a3;
+    }
+    for (; r < rows; r += 4) t += p[(int64_t)r * c];
   }
-  out[i] = t;
+  red[rg][cl] = t;
+  __syncthreads();
+  if (rg == 0 && ch < c) {
+    float s = red[0][cl] + red[1][cl];
+    s += red[2][cl];
+    s += red[3][cl];
+    const int64_t i = (int64_t)nn * c + ch;
+    if (den != nullptr) {
+      const float d = den[i];
+      s = d != 0.f ? s / d : 0.f;
+    }
+    out[i] = s;
+  }
 }
 
 extern "C" int ic2_colsum_div(const float* part, int n, int rows, int c, const float* den, float* out, void* stream) {
-  IC2_CHECK_ARG(part && out && n > 0 && rows > 0 && c > 0 && (int64_t)n * c < (1LL << 31), "colsum_div: bad arguments");
-  const int nc = n * c;
-  hipLaunchKernelGGL(colsum_div_kernel, dim3((unsigned)ceil_div(nc, 256)), dim3(256), 0, as_stream(stream), part, rows,
-                     c, nc, den, out);
+  IC2_CHECK_ARG(part && out && n > 0 && n <= 65535 && rows > 0 && c > 0, "colsum_div: bad arguments");
+  hipLaunchKernelGGL(colsum_div_kernel, dim3((unsigned)ceil_div(c, 64), (unsigned)n), dim3(256), 0, as_stream(stream),
+                     part, rows, c, den, out);
   IC2_CHECK_LAUNCH("colsum_div");
   return IC2_OK;
 }
@@ -902,7 +926,10 @@ extern "C" int ic2_gn_lrelu_pool_bwd_db(const void* y, const void* dout, void* d
                        nchunks, ab);                                                                             \
     const int ng_th = n * groups > c ? n * groups : c;                                                           \
     hipLaunchKernelGGL(gnb_group_kernel, dim3((unsigned)ceil_div(ng_th, 256)), dim3(256), 0, s, ab, n, c_p, c,     \
-                       groups, ng, gamma, stats, (double)h * w, s12, dgamma, dbeta, dsum);                       \
+                       groups, ng, gamma, s12, dgamma, dbeta);                                                   \
+    if (dsum)                                                                                                    \
+      hipLaunchKernelGGL(gnb_dsum_kernel, dim3((unsigned)ceil_div(c, 256)), dim3(256), 0, s, ab, n, c_p, c, groups, \
+                         gamma, stats, s12, (double)h * w, dsum);                                                \
     if (dtype_dy == IC2_F32)                                                                                     \
       hipLaunchKernelGGL((gnb_apply_kernel<TY, TD, float>), apply_grid, dim3(256), 0, s, (const TY*)y,             \
                          (const TD*)dout, (float*)dy, n, h, w, c_p, c, groups, stats, gamma, beta, slope, pool,    \

@@ -173,9 +173,11 @@ def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
     nv.call("ic2_gn_lrelu_pool_bwd_db", nv.ptr(yn), nv.ptr(dn), nv.ptr(dy), nv.dtype_code(dtype), nv.dtype_code(dtype),
             nv.dtype_code(dtype), n, h, w, c_p, c, groups, nv.ptr(stats), nv.ptr(g32), nv.ptr(b32), 0.2, int(pool), None,
             None, nv.ptr(dsum), nv.ptr(ws), wsf, st)
+    # (with one channel per group the per-channel sum is exactly 0: bound the error by the size of the terms)
     ref_sum = yr.grad.sum(dim=(0, 2, 3))
-    assert _rel(dsum, ref_sum) < tol, (_rel(dsum, ref_sum), dtype)
-    assert _rel(dsum, dy.float()[..., :c].sum(dim=(0, 1, 2)).double()) < tol
+    scale = float(yr.grad.abs().sum(dim=(0, 2, 3)).max())
+    assert float((dsum.cpu().double() - ref_sum).abs().max()) < tol * scale
+    assert float((dsum.double() - dy.float()[..., :c].sum(dim=(0, 1, 2)).double()).abs().max()) < tol * scale
 
 
 # ================================================================ synthesis backward (the frozen generator)
