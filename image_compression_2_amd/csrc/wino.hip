@@ -81,6 +81,11 @@ __device__ __forceinline__ int wx_hoff(int line, int hp, int idx, int chunk) {
 #ifndef IC2_WX_SCHED
 #define IC2_WX_SCHED 0
 #endif
+// wave priority A/B (diagnostic builds, tools/build_abl.sh winoprio): 0 = s_setprio 1 over the M section's MFMAs
+// (default), 1 = no s_setprio, 2 = s_setprio 1 over the R section (reads, V adds, DMA issue) instead
+#ifndef IC2_WX_PRIO
+#define IC2_WX_PRIO 0
+#endif
 
 __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[WX_LDS];
@@ -264,6 +269,7 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
           if (j >= 4) issue_hp(cb + 2, j - 4);
         }
       };
+      if constexpr (IC2_WX_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       if constexpr (IC2_WX_SCHED >= 1) r_dma();
       if (hx == 0) make_v();
 #pragma unroll
@@ -299,7 +305,8 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       stamp(3);
       // ---- M section
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (IC2_WX_PRIO == 0) __builtin_amdgcn_s_setprio(1);
+      if constexpr (IC2_WX_PRIO == 2) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int nl = 0; nl < 2; ++nl) {
 #pragma unroll
@@ -317,7 +324,7 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (IC2_WX_PRIO == 0) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (IC2_WX_STAMP) {  // the MFMAs issued (the last one still in the pipe)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
