@@ -253,10 +253,14 @@ class ToNHWC(torch.autograd.Function):
         return dx, None, None
 
 
-def _synth_layer_grads(L, dt, os_, y, dout):
+def _synth_layer_grads(L, dt, os_, y, dout, post=None):
     """Backward of one modulated synthesis layer from dL/d(filtered lrelu output) `dout`: the FLR adjoint stored
     times oscale (dL/dconv) with the per-tile sums for dL/doscale, then the dgrad implicit GEMM -> (dL/da, dL/doscale),
-    a = the conv's (already input-modulated) operand."""
+    a = the conv's (already input-modulated) operand.  post [n][c_p]: `dout` is the gradient of the layer output
+    multiplied by `post` (the next layer's input modulation) and still has to be multiplied by it.  The FLR backward
+    is linear in its input gradient per channel (the lrelu / clamp mask depends on the recomputed U only, the FIRs do
+    not mix channels), so the multiply rides on its per-channel output multiplier: dc = FLRbwd(dout) * oscale * post,
+    and the ydot partials (taken against that multiplier) give dL/doscale = post * sum / oscale."""
     n, h, w, c_p = y.shape
     stream = nv.stream_of(y)
     _, _, bp = L.packed(dt)
@@ -264,6 +268,8 @@ def _synth_layer_grads(L, dt, os_, y, dout):
     px0, px1, py0, py1 = L.padding
     clamp = float(L.conv_clamp) if L.conv_clamp is not None else -1.0
     dc = torch.empty([n, h, w, c_p], dtype=dt, device=y.device)
+    os32 = os_.detach().float()
+    mul = os32 if post is None else (os32 * post).contiguous()
     rc = 2
     if fu is not None and fd is not None and px0 == py0:
         nyd = int(nv.query("ic2_flrelu_bwd_ydot_floats", n, c_p, h, w, L.up_factor))
@@ -272,12 +278,16 @@ def _synth_layer_grads(L, dt, os_, y, dout):
             nv.ptr(y), nv.dtype_code(y.dtype), nv.ptr(dout), nv.dtype_code(dout.dtype), nv.ptr(dc),
             nv.dtype_code(dt), n, c_p, h, w, dout.shape[1], dout.shape[2], fu.ctypes.data_as(ctypes.c_void_p),
             fu.shape[0], fd.ctypes.data_as(ctypes.c_void_p), fd.shape[0], L.up_factor, L.down_factor, px0, px1,
-            py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(os_), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
+            py0, py1, float(L.act_gain), 0.2, clamp, 0, nv.ptr(mul), nv.ptr(bp), nv.ptr(ydot), nyd, stream)
         if rc not in (0, 2):
             raise RuntimeError(f"ic2_flrelu_bwd_nhwc_ex failed: {nv.load().ic2_last_error().decode()}")
     if rc == 0:   # dL/doscale = sum over tiles of the ydot partials / oscale (0 where oscale is 0), one launch
-        d_os = nv.colsum_div(ydot, n, c_p, os_.detach().float())
+        d_os = nv.colsum_div(ydot, n, c_p, os32)
+        if post is not None:
+            d_os = d_os * post
     else:   # no fused instance for this geometry: the composed HIP path + torch epilogue
+        if post is not None:
+            dout = (dout.float() * post[:, None, None, :]).to(dout.dtype)
         gy = _flrelu_backward_composed(y, dout, L)
         dc.copy_(gy * os_[:, None, None, :])
         yd = (gy * (y.float() - bp)).sum(dim=(1, 2))
@@ -340,11 +350,11 @@ class SynthLayerScaledNHWC(torch.autograd.Function):
         n, ho, wo, c_p = out.shape
         npart = int(nv.query("ic2_scale_bwd_part_floats", n, ho * wo, c_p))
         part = torch.empty([npart], dtype=torch.float32, device=out.device)
-        dout = torch.empty_like(out)
-        nv.call("ic2_scale_bwd_nhwc", nv.ptr(g), nv.ptr(out), nv.ptr(xs), nv.ptr(dout), nv.dtype_code(out.dtype), n,
+        # the sums for d xs_next only: g * xs_next itself rides on the FLR backward's output multiplier (post=)
+        nv.call("ic2_scale_bwd_nhwc", nv.ptr(g), nv.ptr(out), nv.ptr(xs), None, nv.dtype_code(out.dtype), n,
                 ho * wo, c_p, nv.ptr(part), npart, nv.stream_of(out))
         d_xs = nv.colsum_div(part, n, c_p, xs)   # sum_p g * out / xs_next, 0 where xs_next = 0
-        da, d_os = _synth_layer_grads(L, dt, os_, y, dout)
+        da, d_os = _synth_layer_grads(L, dt, os_, y, g, post=xs)
         return da, d_os, d_xs, None, None
 
 

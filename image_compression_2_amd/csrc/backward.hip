@@ -668,7 +668,7 @@ __global__ void __launch_bounds__(256) scale_bwd_kernel(const T* __restrict__ da
         const float2 g = sb_ld2(da + e), v = sb_ld2(x + e);
         s0 += g.x * v.x;
         s1 += g.y * v.y;
-        sb_st2(dx + e, make_float2(g.x * sc.x, g.y * sc.y));
+        if (dx != nullptr) sb_st2(dx + e, make_float2(g.x * sc.x, g.y * sc.y));
       }
       sbred[pp * c_p + 2 * cq] = s0;
       sbred[pp * c_p + 2 * cq + 1] = s1;
@@ -737,8 +737,8 @@ extern "C" int ic2_scale_nhwc(const void* x, const float* xscale, void* a, int d
 
 extern "C" int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw,
                                   int c_p, float* part, int64_t part_floats, void* stream) {
-  IC2_CHECK_ARG(da && x && xscale && dx && part && n > 0 && hw > 0 && c_p > 0 && c_p % 2 == 0 && c_p <= 512,
-                "scale_bwd_nhwc: bad arguments");
+  IC2_CHECK_ARG(da && x && xscale && part && n > 0 && hw > 0 && c_p > 0 && c_p % 2 == 0 && c_p <= 512,
+                "scale_bwd_nhwc: bad arguments");  // dx may be null: the partial sums only
   IC2_CHECK_ARG(part_floats >= ic2_scale_bwd_part_floats(n, hw, c_p), "scale_bwd_nhwc: partial buffer too small");
   const int chunk_pix = sb_chunk_pix(n, hw);
   const int nchunks = (int)ceil_div(hw, chunk_pix);

@@ -397,7 +397,8 @@ int ic2_flrelu_bwd_nhwc_ex(const void* x, int x_dtype, const void* gout, int g_d
 
 /* Backward of the synthesis input modulation a = x * xscale[n][c] (SG3 modulated_conv2d's style multiply in the
  * activation-scaling form): dx = da * xscale (NHWC, f32 / bf16) and part[n][chunk][c] = per-chunk sums of da * x
- * (dL/dxscale = sum over chunks).  part: ic2_scale_bwd_part_floats() floats.  Deterministic. */
+ * (dL/dxscale = sum over chunks).  part: ic2_scale_bwd_part_floats() floats.  dx may be NULL (the partial sums only:
+ * the training path folds xscale into the FLR backward's per-channel multiplier instead).  Deterministic. */
 int64_t ic2_scale_bwd_part_floats(int n, int hw, int c_p);
 int ic2_scale_bwd_nhwc(const void* da, const void* x, const float* xscale, void* dx, int dtype, int n, int hw, int c_p,
                        float* part, int64_t part_floats, void* stream);
