@@ -88,7 +88,7 @@ N_CODES = 256               # 8-bit codes: the record's histogram width
 
 CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gnin_gn_fwd", "ic2_from_rgb_conv",
                 "ic2_from_rgb_conv_x3", "ic2_conv_wino")
-TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad",)
+TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad", "ic2_conv_wgrad_oihw")
 FLR_ENTRIES = ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16")
 
 
@@ -131,7 +131,7 @@ class CallTimer:
 
         def call(name, *args):
             f = None
-            if name in CONV_ENTRIES or name == "ic2_conv_wgrad":
+            if name in CONV_ENTRIES or name in ("ic2_conv_wgrad", "ic2_conv_wgrad_oihw"):
                 f, timer.pending = timer.pending, None
             if not timer.enabled or name not in timer.names:
                 return orig(name, *args)
@@ -177,6 +177,10 @@ def conv_call_plan(nv, name, args):
         odt, layout = dt, nv.NHWC
     elif name == "ic2_conv_wgrad":
         dt, (n, h, w, cin_p, cout_p, kh, kw, pad) = args[3], args[4:12]
+        return "conv_wgrad", 2 * n * h * w * cout_p * kh * kw * cin_p
+    elif name == "ic2_conv_wgrad_oihw":   # the same GEMM, written in the parameter's layout
+        dt, (n, h, w, cin_p, cout_p) = args[3], args[4:9]
+        kh, kw, pad = args[11:14]
         return "conv_wgrad", 2 * n * h * w * cout_p * kh * kw * cin_p
     elif name == "ic2_conv_wino":
         # Winograd F(2,3) along x: 4 positions x 3 kernel rows = 12 MFMA products per output pair (the direct conv's

@@ -80,6 +80,7 @@ _SIGS = {
     "ic2_rc_decode": [_P, _P, _I64, _I, _I, _I, _P, _I],
     "ic2_conv_wgrad_ws_floats": [_I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_conv_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I64, _P],
+    "ic2_conv_wgrad_oihw": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I64, _P],
     "ic2_gn_lrelu_pool_bwd_floats": [_I, _I, _I, _I, _I],
     "ic2_gn_lrelu_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _I64,
                               _P],

@@ -155,10 +155,9 @@ class Conv2dNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             nfl = int(nv.query("ic2_conv_wgrad_ws_floats", n, h, w, cin_p, cout_p, kh, kw, ctx.pad))
             ws = torch.empty([max(nfl, 4)], dtype=torch.float32, device=x.device)
-            dwp = torch.empty([cout_p, kh, kw, cin_p], dtype=torch.float32, device=x.device)
-            nv.call("ic2_conv_wgrad", nv.ptr(x), nv.ptr(dy), nv.ptr(dwp), nv.dtype_code(x.dtype), n, h, w, cin_p,
-                    cout_p, kh, kw, ctx.pad, nv.ptr(ws), nfl, nv.stream_of(x))
-            dw = dwp[:cout, :, :, :cin].permute(0, 3, 1, 2).contiguous()
+            dw = torch.empty([cout, cin, kh, kw], dtype=torch.float32, device=x.device)   # the parameter's layout
+            nv.call("ic2_conv_wgrad_oihw", nv.ptr(x), nv.ptr(dy), nv.ptr(dw), nv.dtype_code(x.dtype), n, h, w, cin_p,
+                    cout_p, cout, cin, kh, kw, ctx.pad, nv.ptr(ws), nfl, nv.stream_of(x))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             if colsum is not None:   # the GroupNorm backward's f64 channel sums: no pass over dy
                 db = colsum[0][:cout]

@@ -174,6 +174,21 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     dw[e] = s;
   }
 }
+// the same sums written in nn.Conv2d's weight layout [cout][cin][kh][kw] (valid channels only): the parameter's
+// gradient without a slice + permute copy
+__global__ void __launch_bounds__(256) wgrad_reduce_oihw_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                                int64_t total, int splits, int cin_p, int taps,
+                                                                int cout, int cin) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int i = (int)(e % cin_p);
+    const int64_t ot = e / cin_p;
+    const int t = (int)(ot % taps), o = (int)(ot / taps);
+    if (o >= cout || i >= cin) continue;
+    float s = part[e];
+    for (int k = 1; k < splits; ++k) s += part[(int64_t)k * total + e];
+    dw[((int64_t)o * cin + i) * taps + t] = s;
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // Weight gradient, 16-bit operands (round 4): the same GEMM over pixels with KP-pixel stages, double-buffered LDS
@@ -820,8 +835,26 @@ extern "C" int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int 
   return (int64_t)sp * cout_p * kh * kw * cin_p;
 }
 
+static int conv_wgrad_impl(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
+                           int cout_p, int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream,
+                           int oihw_cout, int oihw_cin);
+
 extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
                               int cout_p, int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream) {
+  return conv_wgrad_impl(x, dy, dw, dtype, n, h, w, cin_p, cout_p, kh, kw, pad, workspace, ws_floats, stream, 0, 0);
+}
+
+extern "C" int ic2_conv_wgrad_oihw(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w,
+                                   int cin_p, int cout_p, int cout, int cin, int kh, int kw, int pad, float* workspace,
+                                   int64_t ws_floats, void* stream) {
+  IC2_CHECK_ARG(cout > 0 && cout <= cout_p && cin > 0 && cin <= cin_p, "conv_wgrad_oihw: bad channel counts");
+  return conv_wgrad_impl(x, dy, dw, dtype, n, h, w, cin_p, cout_p, kh, kw, pad, workspace, ws_floats, stream, cout,
+                         cin);
+}
+
+static int conv_wgrad_impl(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
+                           int cout_p, int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream,
+                           int oihw_cout, int oihw_cin) {
   IC2_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null pointer");
   IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16, "conv_wgrad: bad dtype %d", dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
@@ -866,7 +899,11 @@ extern "C" int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtyp
     else if (dtype == IC2_F16) hipLaunchKernelGGL(wgrad_kernel<_Float16>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, a);
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, s, workspace, dw, total, splits);
+  if (oihw_cout > 0)
+    hipLaunchKernelGGL(wgrad_reduce_oihw_kernel, dim3(grid_for(total)), dim3(256), 0, s, workspace, dw, total, splits,
+                       cin_p, kh * kw, oihw_cout, oihw_cin);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(total)), dim3(256), 0, s, workspace, dw, total, splits);
   IC2_CHECK_LAUNCH("conv_wgrad");
   return IC2_OK;
 }

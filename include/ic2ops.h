@@ -317,6 +317,11 @@ int ic2_rc_decode(const uint8_t* in, const int64_t* stream_bytes, int64_t n_stre
 int64_t ic2_conv_wgrad_ws_floats(int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad);
 int ic2_conv_wgrad(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p, int cout_p,
                    int kh, int kw, int pad, float* workspace, int64_t ws_floats, void* stream);
+/* The same gradient written in nn.Conv2d's weight layout dw [cout][cin][kh][kw] f32 (the parameter's .grad shape,
+ * valid channels only) instead of the packed [cout_p][kh][kw][cin_p]. */
+int ic2_conv_wgrad_oihw(const void* x, const void* dy, float* dw, int dtype, int n, int h, int w, int cin_p,
+                        int cout_p, int cout, int cin, int kh, int kw, int pad, float* workspace, int64_t ws_floats,
+                        void* stream);
 
 /* Backward of ic2_gn_lrelu_pool (VGGBlock :183-191: GroupNorm -> leaky_relu(0.2) -> AvgPool2d(2) when `pool`):
  * y = the GroupNorm input (NHWC [n][h][w][c_p]), stats = ic2_group_norm_stats' output, dout = gradient of the
