@@ -29,7 +29,9 @@ oracle's codes (hvae_training.py:368-395 PSNR, README.md:381 operating point).
 not in the timed value).  --config c5 (BASELINE config 5, the reference's train_hvae_encoder step,
 stylegan3_hvae_full.py:655-707): one optimisation step of the encoder through the frozen synthesis network
 (forward, the reference's second encoder pass for the KL term, backward, data-parallel gradient all_reduce over
-RCCL, Adam); LPIPS excluded (its pretrained VGG weights are not available offline).
+RCCL, Adam); LPIPS excluded (its pretrained VGG weights are not available offline).  The two encoder calls on the
+batch share one trunk and run the projector heads twice (training.train_step shared_trunk: the reference's values
+and RNG draws, one trunk backward for both heads' gradients).
 
 Multi-GPU: one process per GPU, batch-sharded, weak scaling (every rank runs its own batch).  Under torchrun
 the ranks come from the env; `python bench.py --gpus N` without torchrun spawns the N ranks itself
@@ -620,6 +622,8 @@ def run(args):
     elif args.config == "c5":
         out["config"].update(quantization_bits=None, loss="rec MSE + 0.01 KL(w_avg); LPIPS excluded (no weights "
                              "offline)", optimizer="Adam(1e-4, (0.9, 0.999))",
+                             encoder_calls="2 per step as the reference (:669, :678), sharing one trunk "
+                                           "(from_rgb + blocks + GAP) with the projector heads run twice",
                              parallelism=f"dp{world} (batch-sharded, RCCL gradient all_reduce)")
         out["last_step_losses"] = {"rec_loss": round(vec[0].item() / vec[2].item(), 6),
                                    "kl_loss": round(vec[1].item() / vec[2].item(), 4)}

@@ -372,6 +372,13 @@ class HVAE_VGG_Encoder(nn.Module):
     def forward_train(self, x):
         """Autograd path: NHWC activations in the module's precision, HIP forward + backward kernels per op
         ('bf16x3', an inference precision, trains in bf16)."""
+        return self.heads_train(self.trunk_train(x))
+
+    def trunk_train(self, x):
+        """The autograd path's trunk: from_rgb, the blocks (with the reference's 1x1 break) and the global average
+        pools of the three hierarchy features -> {'global', 'medium', 'fine'}: pooled [N, C] f32.  No randomness:
+        two calls on the same input and weights give the same values, so a caller that needs the encoder twice on one
+        batch (the reference's training step, :669 and :678) can run it once and the heads twice."""
         x = x.to(torch.float32)
         nv.require_gpu(x.contiguous())
         dt, _ = nv.encoder_dtype(self.precision)
@@ -391,11 +398,15 @@ class HVAE_VGG_Encoder(nn.Module):
         feats["global"] = (h, c)
         feats.setdefault("fine", (h, c))
         feats.setdefault("medium", (h, c))
+        return {key: ao.GlobalAvgPoolNHWC.apply(*feats[key]) for key in ("global", "medium", "fine")}
+
+    def heads_train(self, pooled):
+        """The three projectors on trunk_train's pooled features, in the reference's order (global, medium, fine:
+        :160-167), each with its fc1 quirk and reparameterisation draw -> (w_plus, means, logvars)."""
         outs = []
         for proj, key in ((self.global_projector, "global"), (self.medium_projector, "medium"),
                           (self.fine_projector, "fine")):
-            fh, fc = feats[key]
-            outs.append(proj.forward_pooled_train(ao.GlobalAvgPoolNHWC.apply(fh, fc)))
+            outs.append(proj.forward_pooled_train(pooled[key]))
         return tuple(torch.cat([o[k] for o in outs], dim=1) for k in range(3))
 
 

@@ -58,14 +58,19 @@ def make_f16(compressor):
 
 
 def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_weight=0.8, kl_weight=0.01,
-               percep=None, second_encoder_pass=True, sync_gradients=None, scaler=None):
+               percep=None, second_encoder_pass=True, sync_gradients=None, scaler=None, shared_trunk=True):
     """One optimisation step; returns the four losses as 0-d device tensors (no host sync).
 
     ``w_avg``: G.mapping.w_avg shaped [1, 1, w_dim] (ref :626).  ``second_encoder_pass=False`` reuses the
     first pass's means / logvars for the KL term (identical values unless the projector's fc1 quirk redraws
     fc1, ref :225-230) and skips one encoder forward.  ``sync_gradients``: world size for the data-parallel
     gradient average (default: the initialised process group's).  ``scaler``: a torch.amp.GradScaler for f16 training
-    (make_f16): scaled backward, then unscale + overflow check + step + scale update, as the reference's :693-696."""
+    (make_f16): scaled backward, then unscale + overflow check + step + scale update, as the reference's :693-696.
+    ``shared_trunk`` (with second_encoder_pass): the reference's two encoder calls on the same batch (:669, :678)
+    share one trunk (from_rgb, blocks, global average pools: deterministic, so both calls compute the same values)
+    and run the projector heads twice in the reference's order -- the second call's fc1 re-draw and
+    reparameterisation draw included, so every value and RNG draw is the reference's.  Autograd then sums both heads'
+    gradients into one trunk backward instead of running two (the same gradient up to summation order)."""
     if percep is None and perceptual_weight != 0:
         raise ValueError("perceptual_weight != 0 needs a perceptual loss callable (the reference's LPIPS(net='vgg') "
                          "weights are not available offline): pass percep=... or perceptual_weight=0")
@@ -79,10 +84,19 @@ def train_step(compressor, images, optimizer, w_avg, rec_weight=1.0, perceptual_
             proj.fc1_hook = icd.broadcast_params
     try:
         return _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight,
-                           percep, second_encoder_pass, sync_gradients, scaler)
+                           percep, second_encoder_pass, sync_gradients, scaler, shared_trunk)
     finally:
         for proj in projectors:
             proj.fc1_hook = None
+
+
+def _decode(compressor, w_plus, images):
+    """compressor.forward after the encoder: the frozen synthesis, resized to the batch's resolution (:669)."""
+    img = compressor.generator.synthesis(w_plus, noise_mode="const")
+    if compressor.training_resolution is not None and img.shape[2] != images.shape[2]:
+        from .stylegan3_hvae_full import resize_bilinear
+        img = resize_bilinear(img, (images.shape[2], images.shape[3]))
+    return img
 
 
 def _reducer(encoder, world):
@@ -100,9 +114,14 @@ def _reducer(encoder, world):
 
 
 def _train_step(compressor, encoder, images, optimizer, w_avg, rec_weight, perceptual_weight, kl_weight, percep,
-                second_encoder_pass, sync_gradients, scaler=None):
+                second_encoder_pass, sync_gradients, scaler=None, shared_trunk=True):
     with torch.enable_grad(), ao.derived_cache():
-        if second_encoder_pass:
+        if second_encoder_pass and shared_trunk:
+            pooled = encoder.trunk_train(images)
+            w_plus, _, _ = encoder.heads_train(pooled)          # compressor(images) (:669)
+            reconstructed = _decode(compressor, w_plus, images)
+            _, means, logvars = encoder.heads_train(pooled)     # encoder(images) (:678)
+        elif second_encoder_pass:
             reconstructed, _ = compressor(images)
             _, means, logvars = encoder(images)
         else:

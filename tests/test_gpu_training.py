@@ -701,3 +701,42 @@ def test_colsum_div_matches_torch_where_chain(cuda):
         assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
         assert (got[:, ::7] == 0).all()
         assert torch.allclose(nv.colsum_div(part, n, c).double(), s, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("precision,gtol", [("fp32", 5e-5), ("f16", 2e-2)])
+def test_train_step_shared_trunk_matches_two_encoder_passes(cuda, precision, gtol):
+    """train_step's shared trunk (the reference's two encoder calls on one batch, :669 and :678, as one trunk and two
+    projector heads) against two full encoder passes: the same losses (every value and RNG draw is the same) and the
+    same gradients up to summation order."""
+    import image_compression_2_amd as ic2
+    from image_compression_2_amd import training as ict
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=64, channel_base=1024, channel_max=64).to(cuda)
+    torch.manual_seed(1)
+    G = ic2.Generator(img_resolution=256).to(cuda).eval().requires_grad_(False)
+    comp = ic2.StyleGAN3Compressor(enc, G, training_resolution=64)
+    scaler = None
+    if precision == "f16":
+        scaler = ict.make_f16(comp)
+    w_avg = G.mapping.w_avg.view(1, 1, -1)
+    x = (torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(cuda)
+    res = {}
+    for shared in (True, False):
+        opt = torch.optim.SGD(enc.parameters(), lr=0.0)   # no update: both runs see the same weights
+        torch.manual_seed(11)
+        out = ict.train_step(comp, x, opt, w_avg, perceptual_weight=0.0, sync_gradients=1, scaler=scaler,
+                             shared_trunk=shared)
+        res[shared] = ({k: float(v) for k, v in out.items()},
+                       {k: p.grad.detach().clone() for k, p in enc.named_parameters() if p.grad is not None})
+    (la, ga), (lb, gb) = res[True], res[False]
+    print(f"[shared trunk {precision}] losses {la} vs {lb}")
+    for k in la:
+        assert abs(la[k] - lb[k]) <= 1e-6 * max(1.0, abs(lb[k])), (k, la[k], lb[k])
+    assert ga.keys() == gb.keys()
+    # a conv followed by a one-channel-per-group GroupNorm has an exactly zero bias gradient (sum of dy over the
+    # group): both runs hold rounding noise there, bounded against the largest gradient instead
+    gmax = max(float(g.norm()) for g in gb.values())
+    errs = sorted(((_rel(ga[k], gb[k]) if float(gb[k].norm()) > 1e-6 * gmax
+                    else float((ga[k] - gb[k]).norm()) / gmax, k) for k in gb), reverse=True)
+    print(f"[shared trunk {precision}] worst gradients {[(k, round(e, 6)) for e, k in errs[:6]]}")
+    assert errs[0][0] < gtol, errs[:6]
