@@ -12,7 +12,7 @@ import json
 import re
 from collections import defaultdict
 
-CONV = ("igemm", "hg4_", "hconv_", "torgb_", "from_rgb")
+CONV = ("igemm", "hg4_", "hconv_", "torgb_", "from_rgb", "wino_fx")
 
 
 def main():
@@ -47,7 +47,7 @@ def main():
     wall = sum((int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) * 1e-6 for a, b in timed) / n
     lines = [f"{args.trace}: {len(steps)} steps, {args.warmup} dropped, {n} timed",
              f"kernel time per step {total:.3f} ms (first dispatch to last of a step: {wall:.3f} ms)",
-             f"conv family per step {conv:.3f} ms (every igemm*/hg4_*/hconv_*/torgb_*/from_rgb* dispatch incl. the "
+             f"conv family per step {conv:.3f} ms (every igemm*/hg4_*/hconv_*/wino_fx*/torgb_*/from_rgb* dispatch incl. the "
              f"split-K combine); median step {med_conv:.3f} ms (per-step conv ms: "
              f"{', '.join(f'{v:.2f}' for v in step_conv)})", f"filtered lrelu per step {flr:.3f} ms"]
     if args.bench:
