@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(256) pack_wino_kernel(const float* __restrict_
 
 // The tile of one launch: th rows x twp pairs, each row served by ns 16-lane pair blocks (th * ns <= 8 blocks,
 // twp <= 16 ns), halo (th + 2) * 2 * (twp + 1) <= WX_HROWS rows; fewest rounds of one workgroup per CU over the chip's
-// 256 CUs, then fewest workgroups.
+// 256 CUs, then fewest workgroups, then full pair blocks.
 struct WxTile {
   int twp, th, ns, hp, nh, tx, ty, to;
   int64_t blocks;
@@ -485,7 +485,11 @@ static WxTile wx_tile(int n, int ho, int wo, int cout_p) {
         t.to = (int)ceil_div(cout_p, WX_BO);
         t.blocks = (int64_t)n * t.tx * t.ty * t.to;
         const int64_t rounds = ceil_div(t.blocks, 256);
-        if (best_rounds < 0 || rounds < best_rounds || (rounds == best_rounds && t.blocks < best.blocks)) {
+        // ties: the fewest workgroups, then full 16-pair blocks (16 x 8 beat 15 x 8 at equal counts by 0.4-1.3 % on
+        // the SG3-T-256 148-px layers, tools/gpu_wxtile.sh)
+        const bool full = twp % 16 == 0, best_full = best.twp % 16 == 0;
+        if (best_rounds < 0 || rounds < best_rounds ||
+            (rounds == best_rounds && (t.blocks < best.blocks || (t.blocks == best.blocks && full && !best_full)))) {
           best = t;
           best_rounds = rounds;
         }
