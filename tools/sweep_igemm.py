@@ -3,7 +3,8 @@
     python tools/sweep_igemm.py [VAR=value,VAR=value ...]   (each argument = one variant, own child process)
 
 Shapes: the 1024-config encoder on 256^2 input (pad 1) and the SG3-T-256 synthesis layers (pad 2).
-Prints one JSON line per variant: {shape: [us, TFLOP/s]}.
+Prints one JSON line per variant: {shape: [us, TFLOP/s]}.  SWEEP_DT=f16: f16 operands and output (the synthesis
+precision of the bench's default mode).
 """
 import json
 import os
@@ -33,19 +34,21 @@ def child(only):
     from image_compression_2_amd import _native as nv
     dev = torch.device("cuda", 0)
     n = 8 if os.environ.get("SWEEP_SET") == "c4" else 32
+    f16 = os.environ.get("SWEEP_DT") == "f16"
+    tdt, code = (torch.float16, nv.F16) if f16 else (torch.bfloat16, nv.BF16)
     res = {}
     for name, ci, co, s, pad in SHAPES:
         if only and name not in only:
             continue
         cip, cop = (nv.pad_synth(ci), nv.pad_synth(co)) if name[0] in "sT" else (nv.pad32(ci), nv.pad32(co))
         ho = s + 2 * pad - 2
-        x = torch.randn(n, s, s, cip, device=dev).to(torch.bfloat16)
-        w = (torch.randn(cop, 3, 3, cip, device=dev) / (9 * cip) ** 0.5).to(torch.bfloat16)
+        x = torch.randn(n, s, s, cip, device=dev).to(tdt)
+        w = (torch.randn(cop, 3, 3, cip, device=dev) / (9 * cip) ** 0.5).to(tdt)
         b = torch.zeros(cop, device=dev)
-        y = torch.empty(n, ho, ho, cop, device=dev, dtype=torch.bfloat16)
+        y = torch.empty(n, ho, ho, cop, device=dev, dtype=tdt)
 
         def run():
-            nv.conv_igemm(nv.ptr(x), nv.ptr(w), nv.ptr(y), nv.BF16, nv.BF16, n, s, s, cip, cop, co, 3, 3, pad, ho, ho,
+            nv.conv_igemm(nv.ptr(x), nv.ptr(w), nv.ptr(y), code, code, n, s, s, cip, cop, co, 3, 3, pad, ho, ho,
                           None, nv.ptr(b), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, nv.stream_of(x), dev)
         for _ in range(3):
             run()
