@@ -89,7 +89,7 @@ HBM_PEAK_GBS = 8000.0
 N_CODES = 256               # 8-bit codes: the record's histogram width
 
 CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gnin_gn_fwd", "ic2_from_rgb_conv",
-                "ic2_from_rgb_conv_x3", "ic2_conv_wino")
+                "ic2_from_rgb_conv_x3", "ic2_from_rgb_conv_f16", "ic2_conv_wino")
 TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad", "ic2_conv_wgrad_oihw")
 FLR_ENTRIES = ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16")
 
@@ -163,7 +163,7 @@ class CallTimer:
 
 def conv_call_plan(nv, name, args):
     """(kernel instance(s) the launch plan ran, MFMA FLOPs it executed incl. channel padding) of one conv call."""
-    if name in ("ic2_from_rgb_conv", "ic2_from_rgb_conv_x3"):
+    if name in ("ic2_from_rgb_conv", "ic2_from_rgb_conv_x3", "ic2_from_rgb_conv_f16"):
         cin, (n, h, w, cout_p) = args[1], args[6:10]
         return name[4:], 2 * n * h * w * cout_p * 9 * cin
     if name == "ic2_conv_igemm_ws":
@@ -174,6 +174,8 @@ def conv_call_plan(nv, name, args):
         odt, layout = dt, nv.NHWC
         if dt == nv.BF16X3:  # split-bf16 encoder: bf16 GEMM over the tripled K, f32 out
             dt, odt = nv.BF16, nv.F32
+        elif dt == nv.F16X2:  # its first blocks: f16 GEMM over the doubled K, f32 out
+            odt = nv.F32
     elif name == "ic2_conv3x3_gnin_gn_fwd":
         dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[5], args[6:15]
         odt, layout = dt, nv.NHWC
@@ -195,7 +197,9 @@ def conv_call_plan(nv, name, args):
     plan = nv.conv_plan(dt, odt, layout, n, h, w, cin_p, cout_p, cv, kh, kw, pad)
     if name == "ic2_conv3x3_gn_fwd" and odt == nv.F32 and plan.startswith("hg4_o"):
         # the split conv with the GroupNorm statistics in its epilogue (igemm.hip x3_gn_hg4: 12-row tiles for 64-wide)
-        plan = "hg4_o64_w32_t12_gn" if plan.startswith("hg4_o64") else plan + "_gn"
+        f16 = plan.endswith("_f16")
+        base = plan[:-4] if f16 else plan
+        plan = ("hg4_o64_w32_t12_gn" if base.startswith("hg4_o64") else base + "_gn") + ("_f16" if f16 else "")
     return plan, 2 * n * ho * wo * cout_p * kh * kw * cin_p
 
 

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libic2ops.so")
 if os.environ.get("IC2_DEV") == "1" and os.environ.get("IC2_DEV_LIB"):
     LIB_PATH = os.environ["IC2_DEV_LIB"]
 
-F32, BF16, F16, BF16X3 = 0, 1, 2, 3
+F32, BF16, F16, BF16X3, F16X2 = 0, 1, 2, 3, 4
 ACT_LINEAR, ACT_LRELU = 0, 1
 NHWC, NCHW, NHWC16 = 0, 1, 2
 
@@ -65,6 +65,7 @@ _SIGS = {
     "ic2_nchw_to_nhwc": [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
     "ic2_from_rgb_conv": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "ic2_from_rgb_conv_x3": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
+    "ic2_from_rgb_conv_f16": [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "ic2_nhwc_to_nchw": [_P, _I, _P, _I, _I, _I, _I, _I, _P],
     "ic2_group_norm_stats_floats": [_I, _I, _I],
     "ic2_group_norm_stats": [_P, _I, _I, _I, _I, _I, _I, _F, _P, _P],

@@ -562,8 +562,9 @@ extern "C" int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c
 // reads).  Arithmetic: bf16 operands, f32 sums (tap order), + bias, one bf16 rounding -- as the MFMA conv.
 // ------------------------------------------------------------------------------------------------
 // X3 (the encoder's split-bf16 mode, ic2_from_rgb_conv_x3): wp is the nn.Conv2d weight itself (f32 [cout][cin][3][3],
-// `cin_p` = cout there), the image is not rounded, and the f32 result is stored split ([hi | lo], 2 * COUT).
-template <int COUT, bool X3 = false>
+// `cin_p` = cout there), the image is not rounded, and the f32 result is stored split ([hi | lo], 2 * COUT); H16
+// (with X3: ic2_from_rgb_conv_f16) stores that f32 result rounded to f16 instead (COUT channels).
+template <int COUT, bool X3 = false, bool H16 = false>
 __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const void* __restrict__ wp,
                                                        int cin_p, const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                        int h, int w, int tiles_x, int tiles_y) {
@@ -619,7 +620,21 @@ __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__
   }
   const int oy = oy0 + py, ox = ox0 + px;
   if (oy >= h || ox >= w) return;
-  if constexpr (X3) {
+  if constexpr (H16) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    uint16_t* yo = reinterpret_cast<uint16_t*>(y) + (((int64_t)nn * h + oy) * w + ox) * COUT;
+#pragma unroll
+    for (int q = 0; q < COUT / 8; ++q) {
+      uint32_t u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = 8 * q + 2 * k;
+        u[k] = __builtin_bit_cast(uint32_t, h2{(_Float16)(acc[o / 2].x + bias[o]), (_Float16)(acc[o / 2].y + bias[o + 1])});
+      }
+      reinterpret_cast<uint4*>(yo)[q] = make_uint4(u[0], u[1], u[2], u[3]);
+    }
+    return;
+  } else if constexpr (X3) {
     bf16_t* yo = y + (((int64_t)nn * h + oy) * w + ox) * 2 * COUT;
 #pragma unroll
     for (int q = 0; q < COUT / 8; ++q) {
@@ -694,6 +709,30 @@ extern "C" int ic2_from_rgb_conv_x3(const float* x, int cin, const float* w, int
     hipLaunchKernelGGL((from_rgb_kernel<128, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
                        (bf16_t*)y, h, w_, tiles_x, tiles_y);
   IC2_CHECK_LAUNCH("from_rgb_conv_x3");
+  return IC2_OK;
+}
+
+extern "C" int ic2_from_rgb_conv_f16(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n,
+                                     int h, int w_, int cout_p, void* stream) {
+  IC2_CHECK_ARG(x && w && bias && y && n > 0 && h > 0 && w_ > 0, "from_rgb_conv_f16: null pointer / bad geometry");
+  IC2_CHECK_ARG(cin >= 1 && cin <= 4 && cout >= 1 && cout <= cout_p && (cout_p == 32 || cout_p == 64 || cout_p == 128),
+                "from_rgb_conv_f16: needs 1 <= cin <= 4, cout <= cout_p, cout_p in {32, 64, 128} (cin=%d cout=%d cout_p=%d)",
+                cin, cout, cout_p);
+  IC2_CHECK_ARG((uintptr_t)y % 16 == 0, "from_rgb_conv_f16: output must be 16-byte aligned");
+  const int tiles_x = (w_ + 31) / 32, tiles_y = (h + 7) / 8;
+  const int64_t blocks = (int64_t)n * tiles_x * tiles_y;
+  IC2_CHECK_ARG(blocks < (1LL << 31), "from_rgb_conv_f16: too many tiles");
+  hipStream_t s = as_stream(stream);
+  if (cout_p == 32)
+    hipLaunchKernelGGL((from_rgb_kernel<32, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  else if (cout_p == 64)
+    hipLaunchKernelGGL((from_rgb_kernel<64, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout, bias,
+                       (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL((from_rgb_kernel<128, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, x, cin, w, cout,
+                       bias, (bf16_t*)y, h, w_, tiles_x, tiles_y);
+  IC2_CHECK_LAUNCH("from_rgb_conv_f16");
   return IC2_OK;
 }
 
@@ -772,8 +811,8 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
                 "conv3x3_gn_fwd: bad arguments");
   // the encoder's precisions only: the fused statistics epilogue and the input-GroupNorm staging are bf16 halo-conv
   // code, and an f16 operand must never reach the bf16 MFMA
-  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_BF16X3,
-                "conv3x3_gn_fwd: dtype must be IC2_F32, IC2_BF16 or IC2_BF16X3");
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_BF16X3 || dtype == IC2_F16X2,
+                "conv3x3_gn_fwd: dtype must be IC2_F32, IC2_BF16, IC2_BF16X3 or IC2_F16X2");
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   IC2_CHECK_ARG(stats_floats >= ic2_conv3x3_gn_stats_floats(dtype, n, h, w_, cin_p, cout_p, kh, kw, pad, groups),
                 "conv3x3_gn_fwd: stats buffer too small");
@@ -784,8 +823,8 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
                                 (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope);
   if (nch == -2) return IC2_E_UNSUPPORTED;
   if (nch < 0) return IC2_E_INVALID;
-  if (nch == 0)  // split-bf16 input: the conv wrote f32
-    return ic2_group_norm_stats(y, dtype == IC2_BF16X3 ? IC2_F32 : dtype, n, ho * wo, cout_p, cout_valid, groups, eps,
+  if (nch == 0)  // split inputs: the conv wrote f32
+    return ic2_group_norm_stats(y, dtype == IC2_BF16X3 || dtype == IC2_F16X2 ? IC2_F32 : dtype, n, ho * wo, cout_p, cout_valid, groups, eps,
                                 stats, stream);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups, nch,
                      (double)ho * wo * (cout_valid / groups), eps, stats);
@@ -882,6 +921,7 @@ extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dty
   else if (dtype_in == IC2_BF16 && dtype_out == IC2_F32) IC2_GN_LAUNCH(bf16_t, float);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16) IC2_GN_LAUNCH(float, bf16_t);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16X3) IC2_GN_LAUNCH(float, bf16x3_t);
+  else if (dtype_in == IC2_F32 && dtype_out == IC2_F16) IC2_GN_LAUNCH(float, _Float16);
   else if (dtype_in == IC2_F16 && dtype_out == IC2_F16) IC2_GN_LAUNCH(_Float16, _Float16);
   else IC2_CHECK_ARG(false, "gn_lrelu_pool: bad dtypes");
 #undef IC2_GN_LAUNCH

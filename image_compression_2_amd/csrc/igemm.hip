@@ -973,6 +973,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 hg4_o64_w32_t12_gn_kernel(IgemmArgs a, int tx, int ty) {
   hg4_body<4, 6, 1, 4, 32, 4, true, false, 2, true>(a, tx, ty);
 }
+// the same three with f16 operands: the split encoder's first blocks (IC2_F16X2: f16 input, [hi | lo] f16 weights)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o64_w32_p3_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
+  hg4_body<4, 4, 1, 4, 32, 6, true, true, 3, true>(a, tx, ty);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o128_w32_p2_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
+  hg4_body<8, 4, 1, 4, 32, 4, true, true, 2, true>(a, tx, ty);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+hg4_o64_w32_t12_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
+  hg4_body<4, 6, 1, 4, 32, 4, true, true, 2, true>(a, tx, ty);
+}
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_P
 
@@ -1060,7 +1073,7 @@ struct IgPlan {
   int tile, bo, bp, splits;
 };
 
-static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int kw, int64_t x_elems) {
+static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int kw, int64_t x_elems, bool x8 = true) {
   static const int BOs[8] = {128, 256, 32, 128, 128, 64, 256, 128};
   static const int BPs[8] = {128, 256, 256, 256, 128, 256, 256, 512};
   static const int forced = knob("IC2_IGEMM_TILE", 0);
@@ -1082,7 +1095,7 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     // bench shapes, tools/sweep_igemm.py): 256 x 256 for cout_p > 128 (padded 64-row quadrants skip their
     // MFMAs) unless cout_p is an odd multiple of 128 (384: the 128 x 512 tile pads nothing), 128 x 512 for
     // 64 < cout_p <= 128; cout_p = 64 keeps the 64 x 256 tile
-    const bool fits8 = cin_p % 64 == 0 && kh * kw <= 32 && x_elems * 2 < (int64_t)kOob &&
+    const bool fits8 = x8 && cin_p % 64 == 0 && kh * kw <= 32 && x_elems * 2 < (int64_t)kOob &&
                        (int64_t)cout_p * K * 2 < (int64_t)kOob;
     const bool odd128 = cout_p % 256 == 128 && cout_p > 128;
     // small grids (the encoder's 512-wide blocks at <= 32^2): the same 8-phase tiles with K split over
@@ -1497,8 +1510,12 @@ static void launch_hconv_cfg(const IgemmArgs& a, hipStream_t s, int cin_p, int c
 // The launch plan of ic2_conv_igemm_ws, in one place: the dispatcher, the workspace query and the plan-name query
 // (tests / bench) all read it, so what is tested and timed is what runs.
 // stored elements per input pixel: the split-bf16 input (IC2_BF16X3, cin_p = the GEMM's tripled K channels) is
-// stored [hi | lo], 2/3 of them
-static int x_pix_of(int dtype, int cin_p) { return dtype == IC2_BF16X3 ? cin_p / 3 * 2 : cin_p; }
+// stored [hi | lo], 2/3 of them; the f16 input of the split-weight mode (IC2_F16X2, cin_p = the doubled K) half
+static int x_pix_of(int dtype, int cin_p) {
+  return dtype == IC2_BF16X3 ? cin_p / 3 * 2 : dtype == IC2_F16X2 ? cin_p / 2 : cin_p;
+}
+// 32-channel blocks of the stored input the split K runs over twice (hi, hi) / once more (x, x) (0: plain input)
+static int x_hb32_of(int dtype, int cin_p) { return dtype == IC2_BF16X3 ? cin_p / 96 : dtype == IC2_F16X2 ? cin_p / 64 : 0; }
 
 enum ConvKind { CK_TORGB, CK_HG4, CK_HCONV, CK_IGEMM };
 struct ConvChoice {
@@ -1513,11 +1530,13 @@ static ConvChoice conv_choice(int dtype, int out_layout, int out_dtype, int n, i
   const int64_t M = (int64_t)n * ho * wo;
   const int64_t x_elems = (int64_t)n * h * w_ * x_pix_of(dtype, cin_p);  // stored elements (buffer-offset limits)
   ConvChoice c;
-  // the split-bf16 input ([hi | lo] storage) runs on the kernels whose input addressing maps the tripled K onto it
-  // (implicit GEMM, 8-phase, hg4) and is planned as the bf16 GEMM over the tripled K
-  const bool x3 = dtype == IC2_BF16X3;
-  if (x3) dtype = IC2_BF16;
-  c.pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, x_elems);
+  // the split inputs (IC2_BF16X3 [hi | lo] storage, IC2_F16X2 plain f16) run on the kernels whose input addressing
+  // maps the tripled / doubled K onto them (implicit GEMM, 8-phase, hg4), planned as the 16-bit GEMM over that K.
+  // The 8-phase kernels address 64-channel K blocks: the doubled K needs an even number of stored 32-channel blocks
+  const bool x3 = dtype == IC2_BF16X3 || dtype == IC2_F16X2;
+  const bool x8 = dtype != IC2_F16X2 || (cin_p / 2) % 64 == 0;
+  if (x3) dtype = dtype == IC2_F16X2 ? IC2_F16 : IC2_BF16;
+  c.pl = ig_plan(dtype, M, cout_p, cin_p, kh, kw, x_elems, x8);
   c.split384 = false;
   if (!x3 && torgb_eligible(dtype, cin_p, cout_valid, kh, kw, pad, out_layout, out_dtype)) {
     c.kind = CK_TORGB;
@@ -1592,7 +1611,7 @@ extern "C" const char* ic2_conv_plan(int dtype, int out_dtype, int out_layout, i
   const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
   const ConvChoice c = conv_choice(dtype, out_layout, out_dtype, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
   const char* name = conv_choice_name(c, dtype, nc, ho, wo, cin_p, cout_p);
-  if (dtype != IC2_F16) return name;
+  if (dtype != IC2_F16 && dtype != IC2_F16X2) return name;
   static thread_local char f16_name[80];  // the f16-operand instance of the same kernel
   snprintf(f16_name, sizeof(f16_name), "%s_f16", name);
   return f16_name;
@@ -1613,10 +1632,12 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                                  float clamp, float out_mul, int out_layout, void* workspace, int64_t ws_bytes,
                                  void* stream) {
   IC2_CHECK_ARG(x && w && y, "conv_igemm: null pointer");
-  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16 || dtype == IC2_BF16X3,
+  IC2_CHECK_ARG(dtype == IC2_F32 || dtype == IC2_BF16 || dtype == IC2_F16 || dtype == IC2_BF16X3 || dtype == IC2_F16X2,
                 "conv_igemm: bad dtype %d", dtype);
   IC2_CHECK_ARG(dtype != IC2_BF16X3 || (cin_p % 96 == 0 && out_layout == IC2_LAYOUT_NHWC),
                 "conv_igemm: split-bf16 input needs cin_p = 3 x a multiple of 32 and NHWC output (cin_p=%d)", cin_p);
+  IC2_CHECK_ARG(dtype != IC2_F16X2 || (cin_p % 64 == 0 && out_layout == IC2_LAYOUT_NHWC),
+                "conv_igemm: split-weight f16 input needs cin_p = 2 x a multiple of 32 and NHWC output (cin_p=%d)", cin_p);
   IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
                 "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
@@ -1657,8 +1678,8 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
   a.in_gn = nullptr; a.in_slope = 0.f;
   a.x_pix = x_pix_of(dtype, cin_p);
-  a.x_hb32 = dtype == IC2_BF16X3 ? cin_p / 96 : 0;
-  const int kdt = dtype == IC2_BF16X3 ? IC2_BF16 : dtype;  // the kernels' operand type
+  a.x_hb32 = x_hb32_of(dtype, cin_p);
+  const int kdt = dtype == IC2_BF16X3 ? IC2_BF16 : dtype == IC2_F16X2 ? IC2_F16 : dtype;  // the kernels' operand type
   static const int group = [] {
     const int g = knob("IC2_IGEMM_GROUP", 1);  // 1 = o-tiles of a p-tile side by side (measured best)
     return g >= 1 ? g : 1;
@@ -1711,15 +1732,15 @@ bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p
 
 static int conv_chunk_n(int dtype, int n, int h, int w_, int cin_p);
 
-// split-bf16 (IC2_BF16X3) conv with f32 output: the hg4 instance the plan picks (per chunk of images, as
+// split-bf16 (IC2_BF16X3) / split-weight f16 (IC2_F16X2) conv with f32 output: the hg4 instance the plan picks (per chunk of images, as
 // ic2_conv_igemm_ws launches it) carries the statistics in its epilogue when it is a 32-wide-tile o64 / o128 kernel
 // over exactly 32 groups of 2 / 4 channels
-static bool x3_gn_hg4(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int groups,
-                      H4Plan* plan) {
+static bool x3_gn_hg4(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                      int groups, H4Plan* plan) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (ho <= 0 || wo <= 0 || groups != 32 || cout_valid != cout_p || (cout_p != 64 && cout_p != 128)) return false;
-  const int nc = conv_chunk_n(IC2_BF16X3, n, h, w_, cin_p);
-  const ConvChoice c = conv_choice(IC2_BF16X3, IC2_LAYOUT_NHWC, IC2_F32, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
+  const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
+  const ConvChoice c = conv_choice(dtype, IC2_LAYOUT_NHWC, IC2_F32, nc, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad);
   if (c.kind != CK_HG4) return false;
   const H4Plan p = h4_plan(nc, ho, wo, cout_p);
   if (!p.tw32 || p.bo != cout_p) return false;
@@ -1732,9 +1753,9 @@ static int x3_gn_th(int cout_p) {
   static const bool t12 = knob("IC2_X3_GN_T12", 1) != 0;
   return cout_p == 64 && t12 ? 12 : 8;
 }
-static int64_t x3_gn_part_doubles(int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
-                                  int groups) {
-  if (!x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr)) return 0;
+static int64_t x3_gn_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw,
+                                  int pad, int groups) {
+  if (!x3_gn_hg4(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr)) return 0;
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   return (int64_t)n * groups * ceil_div(wo, 32) * ceil_div(ho, x3_gn_th(cout_p)) * 2;  // the kernel's 32-wide tiles
 }
@@ -1742,9 +1763,9 @@ static int64_t x3_gn_part_doubles(int n, int h, int w_, int cin_p, int cout_p, i
 bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
                    int groups, int fuse_mode) {
   static const bool x3_env = knob("IC2_X3_GN", 1) == 1;  // A/B: 0 = the separate statistics pass by default
-  if (dtype == IC2_BF16X3)
+  if (dtype == IC2_BF16X3 || dtype == IC2_F16X2)
     return (fuse_mode > 0 || (fuse_mode < 0 && x3_env)) &&
-           x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr);
+           x3_gn_hg4(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, nullptr);
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (ho <= 0 || wo <= 0) return false;
   static const bool fuse_env = knob("IC2_CONV_GN", 0) == 1;
@@ -1760,19 +1781,19 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
                   const float* in_gn, float in_slope) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
-  if (dtype == IC2_BF16X3) {
+  if (dtype == IC2_BF16X3 || dtype == IC2_F16X2) {
     // default on: the statistics epilogue of the non-persistent hg4 costs less than the separate f32 pass saves
     H4Plan p;
     const bool fuse = conv_gn_fuses(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, fuse_mode) &&
                       in_gn == nullptr && bias != nullptr && part != nullptr &&
-                      x3_gn_hg4(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, &p) &&
-                      part_doubles >= x3_gn_part_doubles(n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups);
+                      x3_gn_hg4(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, &p) &&
+                      part_doubles >= x3_gn_part_doubles(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups);
     if (in_gn != nullptr) {
-      set_error("conv3x3_gnin_gn_fwd: no input GroupNorm fusion in split-bf16 mode");
+      set_error("conv3x3_gnin_gn_fwd: no input GroupNorm fusion in the split modes");
       return -2;
     }
     if (!fuse) {
-      const int rc = ic2_conv_igemm_ws(x, w, y, IC2_BF16X3, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
+      const int rc = ic2_conv_igemm_ws(x, w, y, dtype, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
                                        ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace,
                                        ws_bytes, s);
       return rc == IC2_OK ? 0 : -1;
@@ -1787,9 +1808,10 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;
     a.in_gn = nullptr; a.in_slope = 0.f;
-    a.x_pix = x_pix_of(IC2_BF16X3, cin_p);
-    a.x_hb32 = cin_p / 96;
-    const int nc = conv_chunk_n(IC2_BF16X3, n, h, w_, cin_p);
+    a.x_pix = x_pix_of(dtype, cin_p);
+    a.x_hb32 = x_hb32_of(dtype, cin_p);
+    const bool f16 = dtype == IC2_F16X2;
+    const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
     const int64_t ntile = ceil_div(wo, 32) * ceil_div(ho, x3_gn_th(cout_p));
     for (int i0 = 0; i0 < n; i0 += nc) {  // chunks of whole images (< 2^31 input bytes per launch)
       const int cnt = n - i0 < nc ? n - i0 : nc;
@@ -1798,9 +1820,10 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
       a.gn_part = part + (int64_t)i0 * groups * ntile * 2;
       a.n = cnt;
       a.M = (int)((int64_t)cnt * ho * wo);
-      if (p.bo == 64 && x3_gn_th(64) == 12) launch_hg4<4, 6, 1, 4, 32>(a, s, hg4_o64_w32_t12_gn_kernel);
-      else if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, hg4_o64_w32_p3_gn_kernel);
-      else launch_hg4<8, 4, 1, 4, 32>(a, s, hg4_o128_w32_p2_gn_kernel);
+      if (p.bo == 64 && x3_gn_th(64) == 12)
+        launch_hg4<4, 6, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_t12_gn_kernel_f16 : hg4_o64_w32_t12_gn_kernel);
+      else if (p.bo == 64) launch_hg4<4, 4, 1, 4, 32>(a, s, f16 ? hg4_o64_w32_p3_gn_kernel_f16 : hg4_o64_w32_p3_gn_kernel);
+      else launch_hg4<8, 4, 1, 4, 32>(a, s, f16 ? hg4_o128_w32_p2_gn_kernel_f16 : hg4_o128_w32_p2_gn_kernel);
     }
     return (int)ntile;
   }
@@ -1855,7 +1878,8 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
 
 int64_t conv_gn_fused_part_doubles(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad,
                                    int groups) {
-  if (dtype == IC2_BF16X3) return x3_gn_part_doubles(n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad, groups);
+  if (dtype == IC2_BF16X3 || dtype == IC2_F16X2)
+    return x3_gn_part_doubles(dtype, n, h, w_, cin_p, cout_p, cout_p, kh, kw, pad, groups);
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   if (dtype != IC2_BF16 || !hconv_eligible(dtype, (int64_t)n * ho * wo, cin_p, cout_p, kh, kw)) return 0;
   const int th = cin_p > 64 ? 4 : 8;

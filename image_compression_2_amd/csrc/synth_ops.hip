@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) fc_kernel(const float* __restrict__ x, in
 // ------------------------------------------------------------------------------------------------
 // weight packing [cout][cin][kh][kw] f32 -> [cout_p][kh][kw][cin_p] (dtype); optional pre-normalisation
 // ------------------------------------------------------------------------------------------------
-template <typename T, bool X3 = false>
+template <typename T, bool X3 = false, bool H2 = false>
 __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int kh,
                                                           int kw, int cout_p, int cin_p, int prenorm, float gscale,
                                                           T* __restrict__ out, float* __restrict__ wsq) {
@@ -171,7 +171,13 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
     const int k = e / cin_p;
     float v = 0.f;
     if (o < cout && i < cin) v = w[((int64_t)o * cin + i) * kk + k] * scale * gscale;
-    if constexpr (X3) {
+    if constexpr (H2) {
+      // split-weight f16: [hi | lo] along the doubled channel axis of tap k (ic2ops.h IC2_F16X2)
+      _Float16* row = reinterpret_cast<_Float16*>(out) + ((int64_t)o * kk + k) * 2 * cin_p + i;
+      const _Float16 hi = (_Float16)v;
+      row[0] = hi;
+      row[cin_p] = (_Float16)(v - (float)hi);
+    } else if constexpr (X3) {
       // split bf16: [hi | lo | hi] along the tripled channel axis of tap k (ic2ops.h IC2_BF16X3)
       bf16_t* row = reinterpret_cast<bf16_t*>(out) + ((int64_t)o * kk + k) * 3 * cin_p + i;
       const bf16_t hi = f2bf(v);
@@ -512,6 +518,9 @@ extern "C" int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw
   else if (dtype == IC2_BF16X3)
     hipLaunchKernelGGL((pack_weight_kernel<bf16_t, true>), dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw, cout_p,
                        cin_p, prenorm, scale, (bf16_t*)w_out, wsq_out);
+  else if (dtype == IC2_F16X2)
+    hipLaunchKernelGGL((pack_weight_kernel<_Float16, false, true>), dim3(cout_p), dim3(256), 0, s, w, cout, cin, kh, kw,
+                       cout_p, cin_p, prenorm, scale, (_Float16*)w_out, wsq_out);
   else
     IC2_CHECK_ARG(false, "pack_weight: bad dtype %d", dtype);
   IC2_CHECK_LAUNCH("pack_weight");

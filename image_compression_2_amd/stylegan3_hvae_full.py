@@ -35,39 +35,49 @@ def _version_key(*tensors):
 
 class _Act:
     """NHWC activation handle: tensor [n, h, w, c_p] + logical channel count.  x3: split bf16 (ic2ops.h
-    IC2_BF16X3), the tensor holds 2 * c_p bf16 channels [hi | lo] per pixel (the convs' K runs over [hi | hi | lo])."""
-    __slots__ = ("t", "n", "h", "w", "c", "c_p", "x3")
+    IC2_BF16X3), the tensor holds 2 * c_p bf16 channels [hi | lo] per pixel (the convs' K runs over [hi | hi | lo]).
+    h2: plain f16, consumed by the split-weight convs (IC2_F16X2: K runs over [x | x] against [w_hi | w_lo])."""
+    __slots__ = ("t", "n", "h", "w", "c", "c_p", "x3", "h2")
 
-    def __init__(self, t, c, x3=False):
+    def __init__(self, t, c, x3=False, h2=False):
         self.t = t
         self.n, self.h, self.w, cp = t.shape
         self.c_p = cp // 2 if x3 else cp
         self.c = c
         self.x3 = x3
+        self.h2 = h2
+
+    @property
+    def split(self):
+        return self.x3 or self.h2
 
     @property
     def k_p(self):
-        """Channel stride the conv's GEMM sees (the tripled one in split mode)."""
-        return 3 * self.c_p if self.x3 else self.c_p
+        """Channel stride the conv's GEMM sees (the tripled / doubled one in the split modes)."""
+        return 3 * self.c_p if self.x3 else 2 * self.c_p if self.h2 else self.c_p
 
     @property
     def code(self):
-        return nv.BF16X3 if self.x3 else nv.dtype_code(self.t.dtype)
+        return nv.BF16X3 if self.x3 else nv.F16X2 if self.h2 else nv.dtype_code(self.t.dtype)
 
 
 def _packed(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
     cout, cin, kh, kw = conv.weight.shape
     assert conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and cin == x.c
-    x3 = bool(getattr(x, "x3", False))
-    key = (dt, x3, _version_key(conv.weight, conv.bias))
+    x3, h2 = bool(getattr(x, "x3", False)), bool(getattr(x, "h2", False))
+    key = (dt, x3, h2, _version_key(conv.weight, conv.bias))
     hit = cache.get(id(conv))
     if hit is None or hit[0] != key:
         w = conv.weight.detach().to(torch.float32).contiguous()
         cout_p, cin_p = nv.pad32(cout), x.c_p
-        # split mode: [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi] against the activation's [hi | hi | lo]
-        wp = torch.empty([cout_p, kh, kw, 3 * cin_p if x3 else cin_p], dtype=dt, device=w.device)
+        # split modes: [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi] against the activation's [hi | hi | lo]; f16
+        # [cout_p][kh][kw][2 * cin_p] = [hi | lo] against [x | x]
+        if h2:
+            wp = torch.empty([cout_p, kh, kw, 2 * cin_p], dtype=torch.float16, device=w.device)
+        else:
+            wp = torch.empty([cout_p, kh, kw, 3 * cin_p if x3 else cin_p], dtype=dt, device=w.device)
         nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(wp),
-                nv.BF16X3 if x3 else nv.dtype_code(dt), None, stream)
+                nv.BF16X3 if x3 else nv.F16X2 if h2 else nv.dtype_code(dt), None, stream)
         bp = torch.zeros([cout_p], dtype=torch.float32, device=w.device)
         if conv.bias is not None:
             bp[:cout] = conv.bias.detach().float()
@@ -98,24 +108,37 @@ def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
 
 # knob IC2_FROM_RGB_DIRECT=0 (IC2_DEV=1) keeps the packing + implicit-GEMM from_rgb (A/B switch)
 _FROM_RGB_DIRECT = nv.knob("IC2_FROM_RGB_DIRECT", 1) != 0
+# knob IC2_SPLIT_F16_BLOCKS: in the split ('bf16x3') mode the first K blocks' convs take f16 activations against
+# split f16 weights (IC2_F16X2, two f16 MFMAs per product instead of three bf16 ones): K = 2 (blocks 0-1,
+# the 1024^2 / 512^2 levels at C4) by default, 0 = every conv split bf16
+_SPLIT_F16_BLOCKS = nv.knob("IC2_SPLIT_F16_BLOCKS", 2)
 # knob IC2_GN_IN_FUSE=1 applies norm1 + lrelu inside conv2's halo-conv staging instead of materialising it.  Bit-identical
 # but measured level on MI355X (C2 1438.0 -> 1439.4, C4 415.5 -> 415.9 img/s, same box: the saved pass is paid back in
 # the heavier staging of the 64-channel halo conv), so off by default
 _GN_IN_FUSE = nv.knob("IC2_GN_IN_FUSE", 0) == 1
 
 
-def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream, split=False):
+def _from_rgb(conv: nn.Conv2d, x, dt, cache: dict, stream, split=False, h2=False):
     """from_rgb on the NCHW f32 image: in bf16 mode one direct kernel (ic2_from_rgb_conv: no 32-channel packed copy
     of the image), else the packing + implicit GEMM.  split: the encoder's bf16x3 mode -- exact f32 arithmetic, the
-    output stored split for the next conv (ic2_from_rgb_conv_x3, or an f32 conv + split packing)."""
+    output stored split for the next conv (ic2_from_rgb_conv_x3, or an f32 conv + split packing); h2: rounded once to
+    f16 instead, the input of a split-weight f16 conv (ic2_from_rgb_conv_f16)."""
     cout, cin, kh, kw = conv.weight.shape
     if split:
         n, _, hh, ww = x.shape
         cout_p = nv.pad32(cout)
         bp = torch.zeros([cout_p], dtype=torch.float32, device=x.device)
         bp[:cout] = conv.bias.detach().float()
+        direct = cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1 and cout_p in (32, 64, 128)
+        if h2 and direct:
+            y = torch.empty([n, hh, ww, cout_p], dtype=torch.float16, device=x.device)
+            wf = conv.weight.detach().to(torch.float32).contiguous()
+            nv.note_flops(_conv_flops(n, hh, ww, cout, cin, 3, 3))
+            nv.call("ic2_from_rgb_conv_f16", nv.ptr(x), cin, nv.ptr(wf), cout, nv.ptr(bp), nv.ptr(y), n, hh, ww,
+                    cout_p, stream)
+            return _Act(y, cout, h2=True)
         y = torch.empty([n, hh, ww, 2 * cout_p], dtype=torch.bfloat16, device=x.device)
-        if cin <= 4 and kh == 3 and kw == 3 and conv.padding[0] == 1 and cout_p in (32, 64, 128):
+        if direct:
             wf = conv.weight.detach().to(torch.float32).contiguous()
             nv.note_flops(_conv_flops(n, hh, ww, cout, cin, 3, 3))
             nv.call("ic2_from_rgb_conv_x3", nv.ptr(x), cin, nv.ptr(wf), cout, nv.ptr(bp), nv.ptr(y), n, hh, ww, cout_p,
@@ -154,24 +177,25 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     wp, bp = _packed(conv, x, dt, cache, stream)
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
-    if x.x3 and bool(nv.query("ic2_conv3x3_gn_fuses", nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw, pad,
-                              norm.num_groups, int(fuse))):
-        # split bf16, 64- / 128-wide layers: the 4-wave halo GEMM writes f32 and the statistics in one launch
+    if x.split and bool(nv.query("ic2_conv3x3_gn_fuses", x.code, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw, pad,
+                                 norm.num_groups, int(fuse))):
+        # split bf16 / split-weight f16, 64- / 128-wide layers: the 4-wave halo GEMM writes f32 and the statistics in
+        # one launch
         y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
-        nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, kh, kw, pad,
+        nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", x.code, x.n, x.h, x.w, x.k_p, cout_p, kh, kw, pad,
                            norm.num_groups))
         stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
-        nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16X3, x.n, x.h, x.w, x.k_p, cout_p, cout,
+        nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, x.n, x.h, x.w, x.k_p, cout_p, cout,
                 kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, None, 0, int(fuse),
                 stream)
         return _Act(y, cout), stats
-    if x.x3:
+    if x.split:
         # split bf16: one bf16 implicit GEMM over the tripled K (its input [hi | lo] read as [hi | hi | lo]), f32 out,
-        # GroupNorm statistics on the f32 values
+        # GroupNorm statistics on the f32 values (split-weight f16: the f16 GEMM over the doubled K)
         y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
-        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), nv.BF16X3, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
+        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
                       pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.t.device)
         ya = _Act(y, cout)
         nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
@@ -221,9 +245,11 @@ def _gn_affine_table(norm: nn.GroupNorm, y: _Act, stats, stream):
     return table
 
 
-def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None, split=False):
+def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope=0.2, stats=None, split=False,
+                      h2=False):
     """nn.GroupNorm -> F.leaky_relu(0.2) (-> AvgPool2d(2, 2)); `stats` from _conv_gn, else computed here.
-    split: f32 arithmetic, output stored split bf16 (the next conv's operand in bf16x3 mode)."""
+    split: f32 arithmetic, output stored split bf16 (the next conv's operand in bf16x3 mode); with h2 rounded once to
+    f16 instead (the operand of a split-weight f16 conv)."""
     groups = norm.num_groups
     if stats is None:
         nfl = int(nv.query("ic2_group_norm_stats_floats", y.n, y.h * y.w, groups))
@@ -231,17 +257,22 @@ def _group_norm_lrelu(norm: nn.GroupNorm, y: _Act, pool: bool, dt, stream, slope
         nv.call("ic2_group_norm_stats", nv.ptr(y.t), nv.dtype_code(y.t.dtype), y.n, y.h * y.w, y.c_p, y.c, groups,
                 float(norm.eps), nv.ptr(stats), stream)
     oh, ow = (y.h // 2, y.w // 2) if pool else (y.h, y.w)
-    out = torch.empty([y.n, oh, ow, 2 * y.c_p if split else y.c_p], dtype=dt, device=y.t.device)
-    nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype),
-            nv.BF16X3 if split else nv.dtype_code(dt), y.n, y.h, y.w, y.c_p, y.c, groups, nv.ptr(stats),
-            nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)
-    return _Act(out, y.c, x3=split)
+    if split and h2:
+        out = torch.empty([y.n, oh, ow, y.c_p], dtype=torch.float16, device=y.t.device)
+        code = nv.F16
+    else:
+        out = torch.empty([y.n, oh, ow, 2 * y.c_p if split else y.c_p], dtype=dt, device=y.t.device)
+        code = nv.BF16X3 if split else nv.dtype_code(dt)
+    nv.call("ic2_gn_lrelu_pool", nv.ptr(y.t), nv.ptr(out), nv.dtype_code(y.t.dtype), code, y.n, y.h, y.w, y.c_p, y.c,
+            groups, nv.ptr(stats), nv.ptr(norm.weight), nv.ptr(norm.bias), float(slope), int(pool), stream)
+    return _Act(out, y.c, x3=split and not h2, h2=split and h2)
 
 
 def _gap(x: _Act, stream):
     nfl = int(nv.query("ic2_global_avg_pool_floats", x.n, x.h * x.w, x.c_p, x.c))
     buf = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
-    nv.call("ic2_global_avg_pool", nv.ptr(x.t), x.code, x.n, x.h * x.w, x.c_p, x.c, nv.ptr(buf), stream)
+    nv.call("ic2_global_avg_pool", nv.ptr(x.t), nv.F16 if x.h2 else x.code, x.n, x.h * x.w, x.c_p, x.c, nv.ptr(buf),
+            stream)
     return buf[: x.n * x.c].view(x.n, x.c)
 
 
@@ -334,12 +365,13 @@ class HVAE_VGG_Encoder(nn.Module):
 
     def features_nhwc(self, x, dt, stream, split=False):
         """from_rgb + blocks with the reference's 1x1 break; returns {'fine','medium','global'} -> _Act."""
-        h = _from_rgb(self.from_rgb, x, dt, self._cache, stream, split=split)
+        nh2 = _SPLIT_F16_BLOCKS if split else 0
+        h = _from_rgb(self.from_rgb, x, dt, self._cache, stream, split=split, h2=nh2 > 0)
         feats = {}
         for i, block in enumerate(self.blocks):
             if h.h <= 1 or h.w <= 1:
                 break
-            h = block.run_nhwc(h, dt, self._cache, stream)
+            h = block.run_nhwc(h, dt, self._cache, stream, h2=i < nh2, h2_next=i + 1 < nh2)
             if i == self.hierarchy_blocks["fine"]:
                 feats["fine"] = h
             elif i == self.hierarchy_blocks["medium"]:
@@ -422,18 +454,20 @@ class VGGBlock(nn.Module):
         self.pool = nn.AvgPool2d(kernel_size=2, stride=2)
         self._cache = {}
 
-    def run_nhwc(self, x: _Act, dt, cache, stream):
-        split = x.x3
+    def run_nhwc(self, x: _Act, dt, cache, stream, h2=False, h2_next=False):
+        """Inference path.  Split mode (x.split): h2 = this block's conv2 takes its input in f16 against split f16
+        weights, h2_next = so does the next block's conv1 (the pooled output stored f16); else split bf16."""
+        split = x.split
         y, st = _conv_gn(self.conv1, self.norm1, x, dt, cache, stream)
         if not split and _gn_in_fusable(self.conv2, y, dt):
             # norm1 + lrelu applied while conv2's halo conv stages its input: lrelu(norm1(y)) never reaches HBM
             y, st = _conv_gn(self.conv2, self.norm2, y, dt, cache, stream,
                              in_gn=(_gn_affine_table(self.norm1, y, st, stream), 0.2))
         else:
-            h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st, split=split)
+            h = _group_norm_lrelu(self.norm1, y, False, dt, stream, stats=st, split=split, h2=h2)
             y, st = _conv_gn(self.conv2, self.norm2, h, dt, cache, stream)
         pool = y.h > 1 and y.w > 1
-        return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st, split=split)
+        return _group_norm_lrelu(self.norm2, y, pool, dt, stream, stats=st, split=split, h2=h2_next)
 
     def forward_train_nhwc(self, h, dt):
         """Autograd path of run_nhwc: (NHWC activation, valid channels) -> the same after the block."""

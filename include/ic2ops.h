@@ -16,6 +16,10 @@
  *     [hi | hi | lo] (the hi block read twice) and accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi in f32: the product
  *     to ~2^-16 relative (the dropped x_lo*w_lo term is ~2^-18) at three bf16 MFMAs -- the encoder's parity mode that
  *     keeps the 8-bit latent indices of the fp32 reference.
+ *   - IC2_F16X2 = 4 (split weights, f16 input, only where an entry point says so): the activation is plain f16 NHWC
+ *     (stride c_p), a packed weight [cout_p][kh][kw][2 * cin_p] f16 = [hi | lo] (lo = f16(w - hi)).  Conv entry
+ *     points take it with cin_p' = 2 * cin_p: K runs over [x | x] and accumulates x*w_hi + x*w_lo in f32 (two f16
+ *     MFMAs; the activation to 2^-11, the weight to ~2^-22).  The split encoder's first blocks.
  *
  * The reference has no native code and no C ABI: each entry point names the Python
  * function of the reference (or of the un-vendored NVlabs/stylegan3 ops it calls) that it replaces.
@@ -31,7 +35,7 @@ extern "C" {
 #endif
 
 enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
-enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2, IC2_BF16X3 = 3 };
+enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2, IC2_BF16X3 = 3, IC2_F16X2 = 4 };
 enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
 /* NHWC16: channel-blocked NHWC, [n][c_p / 16][h][w][16] (the synthesis conv -> fused filtered lrelu hand-off) */
 enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1, IC2_LAYOUT_NHWC16 = 2 };
@@ -139,7 +143,8 @@ int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y
            float w_gain, float b_gain, int act, float alpha, float act_gain, void* stream);
 
 /* Weight packing for the implicit GEMM: w[cout][cin][kh][kw] f32 -> w_out[cout_p][kh][kw][cin_p]
- * (dtype) times `scale`, zero padded; dtype IC2_BF16X3 -> w_out[cout_p][kh][kw][3 * cin_p] bf16 = [hi | lo | hi].
+ * (dtype) times `scale`, zero padded; dtype IC2_BF16X3 -> w_out[cout_p][kh][kw][3 * cin_p] bf16 = [hi | lo | hi],
+ * IC2_F16X2 -> w_out[cout_p][kh][kw][2 * cin_p] f16 = [hi | lo].
  * prenorm != 0 applies modulated_conv2d's w * rsqrt(mean(w^2,[1,2,3]))
  * and writes wsq_out[cout][cin] = sum_k w_norm^2 (nullable).  Called once per weight version. */
 int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
@@ -182,7 +187,9 @@ int ic2_dev_mode(void);
  * Replaces the grouped conv2d of modulated_conv2d [SG3-public] and nn.Conv2d of VGGBlock
  * (stylegan3_hvae_full.py:175-176) / from_rgb (:62).  cin_p, cout_p multiples of 32.  dtype IC2_BF16X3: the
  * split-bf16 input stored [hi | lo] (2/3 * cin_p channels per pixel), cin_p = the tripled K channel count (a multiple
- * of 96), weights from ic2_pack_weight(IC2_BF16X3), NHWC output. */
+ * of 96), weights from ic2_pack_weight(IC2_BF16X3), NHWC output.  dtype IC2_F16X2: the f16 input (cin_p / 2 channels
+ * per pixel), cin_p = the doubled K channel count (a multiple of 64), weights from ic2_pack_weight(IC2_F16X2), NHWC
+ * output. */
 int ic2_conv_igemm(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
                    int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad, int ho, int wo,
                    const float* oscale, const float* bias, int act, float slope, float act_gain, float clamp,
@@ -247,6 +254,10 @@ int ic2_from_rgb_conv(const float* x, int cin, const void* w, int cin_p, const f
  * ([hi | lo], the input layout of the next split-bf16 conv).  cin <= 4, cout <= cout_p, cout_p in {32, 64, 128}. */
 int ic2_from_rgb_conv_x3(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n, int h,
                          int w_, int cout_p, void* stream);
+/* The same exact-f32 from_rgb with the result rounded once to f16 -> y NHWC f16 [n][h][w][cout_p]: the input of an
+ * IC2_F16X2 conv (the split encoder's first block).  cout_p in {32, 64, 128}. */
+int ic2_from_rgb_conv_f16(const float* x, int cin, const float* w, int cout, const float* bias, void* y, int n, int h,
+                          int w_, int cout_p, void* stream);
 
 int ic2_nchw_to_nhwc(const float* x, void* y, int dtype, int n, int c, int h, int w, int c_p, const float* scale,
                      void* stream);
@@ -264,7 +275,8 @@ int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c
 
 /* GroupNorm apply + F.leaky_relu(0.2) (+ AvgPool2d(2,2) when pool != 0), VGGBlock.forward :183-191:
  *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling).  dtype_out may be
- *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][2 * c_p]). */
+ *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][2 * c_p]); dtype_in IC2_F32 -> dtype_out IC2_F16 is the
+ *   input of an IC2_F16X2 conv. */
 int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p, int c,
                       int groups, const float* stats, const float* gamma, const float* beta, float slope,
                       int pool, void* stream);
@@ -354,7 +366,8 @@ int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_
  * at parity on MI355X).  Deterministic.  dtype IC2_BF16X3: the split-bf16 encoder -- x stored
  * [hi | lo] with cin_p = the tripled (GEMM K) channel count, w from ic2_pack_weight(IC2_BF16X3), y f32 NHWC; the
  * statistics come out of the 4-wave halo GEMM's epilogue (on the f32 values as stored) when it runs a 64- / 128-wide
- * layer with 32 groups (fuse != 0), else the separate pass. */
+ * layer with 32 groups (fuse != 0), else the separate pass.  dtype IC2_F16X2: the same with the f16 input and
+ * [hi | lo] f16 weights (cin_p = the doubled K), the f16 instances of those kernels. */
 int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad,
                                     int groups);
 int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,

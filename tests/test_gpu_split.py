@@ -200,3 +200,170 @@ def test_split_global_avg_pool(cuda):
     got = shf._gap(a, nv.stream_of()).cpu().double()
     r = x.double().mean((2, 3))
     assert (got - r).abs().max().item() < 1e-5
+
+
+# ------------------------------------------------------------------------------------------------
+# The split-weight f16 mode of the encoder's first blocks (ic2ops.h IC2_F16X2): f16 activation x, f16 weights
+# w_hi + w_lo, K over [x | x] -> x * w to the f32 accumulation's precision for the f16-rounded x.
+def _h2_pack(x, cuda):
+    """NCHW f32 -> f16 NHWC activation handle for a split-weight conv (ic2_nchw_to_nhwc, dtype IC2_F16)."""
+    n, c, h, w = x.shape
+    c_p = nv.pad32(c)
+    xd = x.to(cuda).contiguous()
+    t = torch.empty([n, h, w, c_p], dtype=torch.float16, device=cuda)
+    nv.call("ic2_nchw_to_nhwc", nv.ptr(xd), nv.ptr(t), nv.F16, n, c, h, w, c_p, None, nv.stream_of(xd))
+    torch.cuda.synchronize()
+    return shf._Act(t, c, h2=True)
+
+
+def test_f16x2_weight_packing(cuda):
+    conv = torch.nn.Conv2d(40, 20, 3, padding=1)
+    a = shf._Act(torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda), 40, h2=True)
+    assert a.k_p == 128 and a.code == nv.F16X2
+    wp, bp = shf._packed(conv.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
+    torch.cuda.synchronize()
+    assert wp.shape == (32, 3, 3, 128) and wp.dtype == torch.float16
+    w = conv.weight.detach().cpu().permute(0, 2, 3, 1)  # [o][ky][kx][i]
+    hi = w.to(torch.float16).float()
+    lo = (w - hi).to(torch.float16).float()
+    got = wp.float().cpu()
+    assert torch.equal(got[:20, ..., :40], hi) and torch.equal(got[:20, ..., 64:104], lo)
+    assert (got[20:] == 0).all() and (got[..., 40:64] == 0).all() and (got[..., 104:] == 0).all()
+
+
+# hg4 (the fused-statistics instances and the plain ones), the generic 16-bit igemm with an odd count of stored
+# 32-channel blocks (the 8-phase kernels need an even one), the 8-phase kernels, small grids with split-K; the
+# last case scales the weights by 1e-3 so that most w_lo are f16 subnormals (the MFMA must not flush them)
+F16X2_CONV_CASES = [(32, 64, 2, 150, 1.0), (64, 64, 2, 129, 1.0), (64, 128, 4, 64, 1.0), (128, 128, 4, 64, 1.0),
+                    (128, 256, 8, 32, 1.0), (256, 512, 8, 16, 1.0), (40, 20, 2, 33, 1.0), (32, 64, 1, 20, 1.0),
+                    (64, 64, 2, 96, 1e-3)]
+
+
+@pytest.mark.parametrize("cin,cout,n,size,wscale", F16X2_CONV_CASES)
+def test_f16x2_conv_gn_matches_fp64(cuda, cin, cout, n, size, wscale):
+    """_conv_gn on an f16 activation (IC2_F16X2): the f32 output within 1e-5 (relative to max |y|) of F.conv2d in
+    fp64 on the f16-rounded activation and the unrounded weights (the weight split carries ~22 bits), and the
+    GroupNorm statistics of that output."""
+    g = torch.Generator().manual_seed(cin * 5 + cout + size)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin) * wscale)
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1 * wscale)
+    norm = torch.nn.GroupNorm(min(32, cout), cout)
+    x = torch.randn(n, cin, size, size, generator=g)
+    a = _h2_pack(x, cuda)
+    plan = nv.conv_plan(nv.F16X2, nv.F32, nv.NHWC, n, size, size, a.k_p, nv.pad32(cout), cout, 3, 3, 1)
+    y, st = shf._conv_gn(conv.to(cuda), norm.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
+    torch.cuda.synchronize()
+    assert y.t.dtype == torch.float32 and not y.split
+    r = F.conv2d(x.to(torch.float16).double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(),
+                 padding=1)
+    got = y.t[..., :cout].cpu().double().permute(0, 3, 1, 2)
+    err = (got - r).abs().max().item() / r.abs().max().item()
+    print(f"[f16x2 conv {cin}->{cout} n{n} {size}^2 w*{wscale:g} plan {plan}] max rel err {err:.2e}")
+    assert err < 1e-5
+    assert (y.t[..., cout:] == 0).all()
+    groups = norm.num_groups
+    rg = r.reshape(n, groups, -1)
+    mean, var = rg.mean(-1), rg.var(-1, unbiased=False)
+    s = st[: n * groups * 2].view(n, groups, 2).cpu().double()
+    assert torch.allclose(s[..., 0], mean, rtol=1e-4, atol=1e-5 * r.abs().max().item())
+    assert torch.allclose(s[..., 1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(32, 64, 8, 126, 124), (64, 128, 8, 126, 124), (64, 64, 8, 1024, 1024),
+                                             (64, 128, 8, 512, 512)])
+def test_f16x2_conv_gn_fused_epilogue(cuda, cin, cout, n, h, w):
+    """The f16 instances of the statistics-epilogue halo GEMMs (hg4_*_gn_kernel_f16): the same f32 output bits as
+    the unfused call and statistics within 1e-6 of the separate pass, on ragged tiles and on the C4 block-0 / block-1
+    conv2 shapes."""
+    g = torch.Generator().manual_seed(cin + cout + h + 1)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1 + 0.05)
+    norm = torch.nn.GroupNorm(32, cout)
+    x = torch.randn(n, cin, h, w, generator=torch.Generator(device=cuda).manual_seed(h), device=cuda)
+    a = _h2_pack(x, cuda)
+    del x
+    assert nv.query("ic2_conv3x3_gn_fuses", nv.F16X2, n, h, w, a.k_p, cout, cout, 3, 3, 1, 32, -1) == 1
+    assert nv.query("ic2_conv3x3_gn_fuses", nv.F16X2, n, h, w, a.k_p, cout, cout, 3, 3, 1, 32, 0) == 0
+    conv, norm = conv.to(cuda), norm.to(cuda)
+    yf, sf = shf._conv_gn(conv, norm, a, torch.bfloat16, {}, nv.stream_of(), fuse=-1)
+    yu, su = shf._conv_gn(conv, norm, a, torch.bfloat16, {}, nv.stream_of(), fuse=0)
+    torch.cuda.synchronize()
+    assert torch.equal(yf.t, yu.t)
+    del yf
+    k = n * 32 * 2
+    sfd, sud = sf[:k].view(n, 32, 2).double(), su[:k].view(n, 32, 2).double()
+    scale = yu.t.abs().max().item()
+    d_mean = (sfd[..., 0] - sud[..., 0]).abs().max().item() / scale
+    d_rstd = ((sfd[..., 1] - sud[..., 1]) / sud[..., 1]).abs().max().item()
+    print(f"[f16x2 conv+GN fused {cin}->{cout} n{n} {h}x{w}] mean {d_mean:.2e} (of max|y|) rstd {d_rstd:.2e} rel")
+    assert d_mean < 1e-6 and d_rstd < 1e-6
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_f16x2_gn_lrelu_pool_f16_out(cuda, pool):
+    """GroupNorm + lrelu (+ pool) in f32 from the f32 conv output, rounded once to f16 (the next split-weight conv's
+    operand): within half an f16 ulp (+ the f32 statistics' ~1e-6) of the fp64 result."""
+    g = torch.Generator().manual_seed(4)
+    n, c, h, w = 3, 64, 18, 14
+    y = torch.randn(n, c, h, w, generator=g) * 2 + 0.3
+    norm = torch.nn.GroupNorm(32, c)
+    with torch.no_grad():
+        norm.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        norm.bias.copy_(torch.randn(c, generator=g))
+    stream = nv.stream_of()
+    ya = shf._to_nhwc(y.to(cuda), torch.float32, stream)
+    out = shf._group_norm_lrelu(norm.to(cuda), ya, pool, torch.bfloat16, stream, split=True, h2=True)
+    assert out.h2 and not out.x3 and out.t.dtype == torch.float16 and out.t.shape[-1] == 64
+    r = F.leaky_relu(F.group_norm(y.double(), 32, norm.weight.detach().cpu().double(),
+                                  norm.bias.detach().cpu().double(), 1e-5), 0.2)
+    if pool:
+        r = F.avg_pool2d(r, 2)
+    got = out.t.float().cpu().double().permute(0, 3, 1, 2)
+    assert ((got - r).abs() <= 2 ** -11 * r.abs() + 1e-5 * (1 + r.abs().max().item())).all()
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(3, 32, 3, 67, 45), (3, 64, 2, 40, 33), (3, 20, 2, 16, 32)])
+def test_from_rgb_f16_out(cuda, cin, cout, n, h, w):
+    """ic2_from_rgb_conv_f16: the exact-f32 from_rgb rounded once to f16 -> within half an f16 ulp of fp64."""
+    g = torch.Generator().manual_seed(cin * 10 + cout + h)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * cin))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    x = torch.rand(n, cin, h, w, generator=g) * 2 - 1
+    a = shf._from_rgb(conv.to(cuda), x.to(cuda), torch.bfloat16, {}, nv.stream_of(), split=True, h2=True)
+    torch.cuda.synchronize()
+    assert a.h2 and a.c == cout and a.t.dtype == torch.float16
+    r = F.conv2d(x.double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(), padding=1)
+    got = a.t[..., :cout].float().cpu().double().permute(0, 3, 1, 2)
+    assert ((got - r).abs() <= 2 ** -11 * r.abs() + 1e-6).all()
+    assert (a.t[..., cout:] == 0).all()
+
+
+def test_split_encoder_first_blocks_run_f16x2(cuda):
+    """The benched split encoder ('bf16x3') runs its first IC2_SPLIT_F16_BLOCKS = 2 blocks' convs as split-weight f16
+    (the f16 statistics-epilogue kernels) and the rest as split bf16."""
+    import image_compression_2_amd as ic2
+    calls = []
+    orig = nv.call
+
+    def rec(name, *args):
+        if name in ("ic2_conv3x3_gn_fwd", "ic2_conv_igemm_ws", "ic2_from_rgb_conv_f16", "ic2_from_rgb_conv_x3"):
+            calls.append((name, args[3] if name in ("ic2_conv3x3_gn_fwd", "ic2_conv_igemm_ws") else None))
+        return orig(name, *args)
+
+    torch.manual_seed(0)
+    enc = ic2.HVAE_VGG_Encoder(img_resolution=1024, precision="bf16x3").to(cuda)
+    x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    nv.call = rec
+    try:
+        enc(x.to(cuda))
+    finally:
+        nv.call = orig
+    assert calls[0] == ("ic2_from_rgb_conv_f16", None)
+    codes = [c for n, c in calls[1:]]
+    assert len(codes) == 16 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}

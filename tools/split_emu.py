@@ -1,6 +1,6 @@
 """CPU emulation of the encoder precision candidates against the fp32 oracle: each conv computed
 in fp64 on operands rounded / split as a mode would store them, conv outputs f32; 8-bit index flips vs the oracle.
-    python tools/split_emu.py B mode [mode ...]   (modes: fp64 bf16 f16 split_bf16 split_f16 x2_* w2_* mixK tailK)"""
+    python tools/split_emu.py B mode [mode ...]   (modes: fp64 bf16 f16 split_bf16 split_f16 x2_* w2_* mixK tailK hmixK)"""
 import sys, torch, torch.nn.functional as F, time
 sys.path.insert(0, '/root/repo')
 import image_compression_2_amd as ic2
@@ -10,7 +10,8 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 torch.manual_seed(0)
 enc = ic2.HVAE_VGG_Encoder(img_resolution=1024)
 sd = {k: v.detach() for k, v in enc.state_dict().items()}
-x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1000)) * 2 - 1
+RES = int(__import__("os").environ.get("RES", "256"))
+x = torch.rand(B, 3, RES, RES, generator=torch.Generator().manual_seed(1000)) * 2 - 1
 torch.manual_seed(5)
 lin = torch.nn.Linear(128, 256); fc1 = (lin.weight.detach(), lin.bias.detach())
 with torch.no_grad():
@@ -25,14 +26,17 @@ CONV_IDX = [0]
 
 def make_conv(mode):
     base = mode
-    if mode.startswith('mix') or mode.startswith('tail'):
+    if mode.startswith('mix') or mode.startswith('tail') or mode.startswith('hmix'):
         # mixK: the first K convs (from_rgb = 0, block i conv1 = 1 + 2i, conv2 = 2 + 2i) in bf16, the rest split;
         # tailK: the convs from index K on in bf16, the ones before split
-        k = int(mode[3:] if mode.startswith('mix') else mode[4:])
+        k = int(mode[4:] if mode.startswith('hmix') else mode[3:] if mode.startswith('mix') else mode[4:])
     def conv(x, w, b):
         mode = base
         if base.startswith('mix'):
             mode = 'bf16' if CONV_IDX[0] < k else 'split_bf16'
+            CONV_IDX[0] += 1
+        elif base.startswith('hmix'):
+            mode = 'w2_f16' if 0 < CONV_IDX[0] < k else 'split_bf16'
             CONV_IDX[0] += 1
         elif base.startswith('tail'):
             mode = 'bf16' if CONV_IDX[0] >= k else 'split_bf16'
@@ -65,6 +69,9 @@ def enc_forward(mode):
     if mode.startswith('mix'):  # activations stored bf16 while the convs consuming them are bf16
         k = int(mode[3:])
         store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] < k else t
+    if mode.startswith('hmix'):  # convs 1 .. K-1 (block 0 = 1, 2) x f16, w split f16; their inputs stored f16
+        k = int(mode[4:])
+        store = lambda t: t.to(torch.float16).float() if 0 < CONV_IDX[0] < k else t
     if mode.startswith('tail'):
         k = int(mode[4:])
         store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] >= k else t
