@@ -98,6 +98,8 @@ _SIGS = {
     "ic2_conv3x3_gn_stats_floats": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_conv3x3_gn_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _F, _P, _I64, _P, _I64, _I,
                            _P],
+    "ic2_conv3x3_gn_fwd_scaled": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _F, _I, _F, _P, _I64, _P,
+                                  _I64, _I, _P],
     "ic2_conv3x3_gnin_supported": [_I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_conv3x3_gn_fuses": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "ic2_gn_affine_table": [_P, _P, _P, _I, _I, _I, _I, _P, _P],

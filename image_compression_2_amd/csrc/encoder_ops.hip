@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(256) resize_bilinear_kernel(const float* __res
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                   int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
                   int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
-                  const float* in_gn, float in_slope);
+                  const float* in_gn, float in_slope, float out_mul = 1.f);
 bool conv_gn_in_supported(int dtype, int n, int h, int w_, int cin_p, int cout_p, int kh, int kw, int pad);
 bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
                    int groups, int fuse_mode);
@@ -806,7 +806,7 @@ extern "C" int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w_, 
 static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
                                int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, int groups,
                                float eps, float* stats, int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes,
-                               int fuse, void* stream, const float* in_gn, float in_slope) {
+                               int fuse, void* stream, const float* in_gn, float in_slope, float out_mul = 1.f) {
   IC2_CHECK_ARG(x && w && y && stats && groups > 0 && cout_valid > 0 && cout_valid % groups == 0,
                 "conv3x3_gn_fwd: bad arguments");
   // the encoder's precisions only: the fused statistics epilogue and the input-GroupNorm staging are bf16 halo-conv
@@ -820,7 +820,7 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
   const int64_t sf = ((int64_t)n * groups * 2 + 1) / 2 * 2;
   double* part = reinterpret_cast<double*>(stats + sf);
   const int nch = conv_gn_fused(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, part,
-                                (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope);
+                                (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope, out_mul);
   if (nch == -2) return IC2_E_UNSUPPORTED;
   if (nch < 0) return IC2_E_INVALID;
   if (nch == 0)  // split inputs: the conv wrote f32
@@ -843,6 +843,16 @@ extern "C" int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dty
                                   int fuse, void* stream) {
   return conv3x3_gn_fwd_impl(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, eps, stats,
                              stats_floats, conv_ws, conv_ws_bytes, fuse, stream, nullptr, 0.f);
+}
+
+extern "C" int ic2_conv3x3_gn_fwd_scaled(const void* x, const void* w, void* y, int dtype, int n, int h, int w_,
+                                         int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
+                                         const float* bias, float out_mul, int groups, float eps, float* stats,
+                                         int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse,
+                                         void* stream) {
+  IC2_CHECK_ARG(dtype == IC2_F16X2 && out_mul > 0.f, "conv3x3_gn_fwd_scaled: IC2_F16X2 with out_mul > 0 only");
+  return conv3x3_gn_fwd_impl(x, w, y, dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, bias, groups, eps, stats,
+                             stats_floats, conv_ws, conv_ws_bytes, fuse, stream, nullptr, 0.f, out_mul);
 }
 
 // (mean, rstd * gamma, beta, 0) per (sample, channel) from GroupNorm stats [n][groups][2] (mean, rstd): the operands

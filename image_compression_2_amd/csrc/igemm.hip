@@ -1778,7 +1778,7 @@ bool conv_gn_fuses(int dtype, int n, int h, int w_, int cin_p, int cout_p, int c
 int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                   int cout_valid, int kh, int kw, int pad, const float* bias, int groups, double* part,
                   int64_t part_doubles, void* workspace, int64_t ws_bytes, int fuse_mode, hipStream_t s,
-                  const float* in_gn, float in_slope) {
+                  const float* in_gn, float in_slope, float out_mul) {
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
   if (dtype == IC2_BF16X3 || dtype == IC2_F16X2) {
@@ -1794,7 +1794,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     }
     if (!fuse) {
       const int rc = ic2_conv_igemm_ws(x, w, y, dtype, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
-                                       ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, 1.f, IC2_LAYOUT_NHWC, workspace,
+                                       ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, out_mul, IC2_LAYOUT_NHWC, workspace,
                                        ws_bytes, s);
       return rc == IC2_OK ? 0 : -1;
     }
@@ -1803,7 +1803,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
     a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
     a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
-    a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = 1.f;
+    a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = out_mul;
     a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = IC2_F32;
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;

@@ -17,6 +17,7 @@ opt-in extension.
 """
 from __future__ import annotations
 
+import math
 import types
 
 import numpy as np
@@ -71,19 +72,29 @@ def _packed(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
         w = conv.weight.detach().to(torch.float32).contiguous()
         cout_p, cin_p = nv.pad32(cout), x.c_p
         # split modes: [cout_p][kh][kw][3 * cin_p] = [hi | lo | hi] against the activation's [hi | hi | lo]; f16
-        # [cout_p][kh][kw][2 * cin_p] = [hi | lo] against [x | x]
+        # [cout_p][kh][kw][2 * cin_p] = [hi | lo] against [x | x], the weights times 2^s (max |w| 2^s in [2^12, 2^13):
+        # the low halves of all but the ~2^-15-smallest weights stay f16 normals), the conv output times 2^-s (exact)
+        mul = 1.0
         if h2:
             wp = torch.empty([cout_p, kh, kw, 2 * cin_p], dtype=torch.float16, device=w.device)
+            m = float(w.abs().max().item())
+            sh = 13 - math.frexp(m)[1] if m > 0 else 0
+            mul = math.ldexp(1.0, -sh)
         else:
             wp = torch.empty([cout_p, kh, kw, 3 * cin_p if x3 else cin_p], dtype=dt, device=w.device)
-        nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0, nv.ptr(wp),
+        nv.call("ic2_pack_weight", nv.ptr(w), cout, cin, kh, kw, cout_p, cin_p, 0, 1.0 / mul, nv.ptr(wp),
                 nv.BF16X3 if x3 else nv.F16X2 if h2 else nv.dtype_code(dt), None, stream)
         bp = torch.zeros([cout_p], dtype=torch.float32, device=w.device)
         if conv.bias is not None:
-            bp[:cout] = conv.bias.detach().float()
-        hit = (key, (wp, bp))
+            bp[:cout] = conv.bias.detach().float() / mul
+        hit = (key, (wp, bp), mul)
         cache[id(conv)] = hit
     return hit[1]
+
+
+def _out_mul(conv: nn.Conv2d, cache: dict):
+    """The output multiplier of conv's cached packing (2^-s for split-weight f16 weights packed times 2^s, else 1)."""
+    return cache[id(conv)][2]
 
 
 def _conv_flops(n, ho, wo, cout, cin, kh, kw):
@@ -186,9 +197,14 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
                            norm.num_groups))
         stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
-        nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, x.n, x.h, x.w, x.k_p, cout_p, cout,
-                kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, None, 0, int(fuse),
-                stream)
+        if x.h2:
+            nv.call("ic2_conv3x3_gn_fwd_scaled", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, x.n, x.h, x.w, x.k_p,
+                    cout_p, cout, kh, kw, pad, nv.ptr(bp), _out_mul(conv, cache), norm.num_groups, float(norm.eps),
+                    nv.ptr(stats), nfl, None, 0, int(fuse), stream)
+        else:
+            nv.call("ic2_conv3x3_gn_fwd", nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, x.n, x.h, x.w, x.k_p, cout_p,
+                    cout, kh, kw, pad, nv.ptr(bp), norm.num_groups, float(norm.eps), nv.ptr(stats), nfl, None, 0,
+                    int(fuse), stream)
         return _Act(y, cout), stats
     if x.split:
         # split bf16: one bf16 implicit GEMM over the tripled K (its input [hi | lo] read as [hi | hi | lo]), f32 out,
@@ -196,7 +212,8 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
         y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
         nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
-                      pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC, stream, x.t.device)
+                      pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, _out_mul(conv, cache), nv.NHWC, stream,
+                      x.t.device)
         ya = _Act(y, cout)
         nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
         stats = torch.empty([nfl], dtype=torch.float32, device=y.device)

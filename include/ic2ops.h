@@ -373,6 +373,13 @@ int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, i
 int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,
                        int cout_valid, int kh, int kw, int pad, const float* bias, int groups, float eps, float* stats,
                        int64_t stats_floats, void* conv_ws, int64_t conv_ws_bytes, int fuse, void* stream);
+/* The same for IC2_F16X2 with the weights packed times a power of two 2^s (ic2_pack_weight's `scale`, so that the
+ * f16 low halves stay normal) and bias [cout_p] times 2^s: y = (conv(x, w) + bias) * out_mul with out_mul = 2^-s,
+ * exact; the statistics are of y. */
+int ic2_conv3x3_gn_fwd_scaled(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p,
+                              int cout_p, int cout_valid, int kh, int kw, int pad, const float* bias, float out_mul,
+                              int groups, float eps, float* stats, int64_t stats_floats, void* conv_ws,
+                              int64_t conv_ws_bytes, int fuse, void* stream);
 /* 1 when ic2_conv3x3_gn_fwd with these arguments takes the statistics from the conv's epilogue (a host query). */
 int ic2_conv3x3_gn_fuses(int dtype, int n, int h, int w, int cin_p, int cout_p, int cout_valid, int kh, int kw, int pad,
                          int groups, int fuse);

@@ -220,20 +220,26 @@ def test_f16x2_weight_packing(cuda):
     conv = torch.nn.Conv2d(40, 20, 3, padding=1)
     a = shf._Act(torch.zeros(1, 4, 4, 64, dtype=torch.float16, device=cuda), 40, h2=True)
     assert a.k_p == 128 and a.code == nv.F16X2
-    wp, bp = shf._packed(conv.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
+    cache = {}
+    wp, bp = shf._packed(conv.to(cuda), a, torch.bfloat16, cache, nv.stream_of())
+    mul = shf._out_mul(conv, cache)
     torch.cuda.synchronize()
     assert wp.shape == (32, 3, 3, 128) and wp.dtype == torch.float16
-    w = conv.weight.detach().cpu().permute(0, 2, 3, 1)  # [o][ky][kx][i]
+    # packed times 2^s = 1 / mul with max |w| 2^s in [2^12, 2^13); the bias likewise
+    w = conv.weight.detach().cpu().permute(0, 2, 3, 1) / mul  # [o][ky][kx][i]
+    assert 2 ** 12 <= w.abs().max().item() < 2 ** 13 and mul == 2.0 ** round(np.log2(mul))
     hi = w.to(torch.float16).float()
     lo = (w - hi).to(torch.float16).float()
     got = wp.float().cpu()
     assert torch.equal(got[:20, ..., :40], hi) and torch.equal(got[:20, ..., 64:104], lo)
     assert (got[20:] == 0).all() and (got[..., 40:64] == 0).all() and (got[..., 104:] == 0).all()
+    assert torch.equal(bp[:20].cpu(), conv.bias.detach().cpu() / mul)
 
 
 # hg4 (the fused-statistics instances and the plain ones), the generic 16-bit igemm with an odd count of stored
 # 32-channel blocks (the 8-phase kernels need an even one), the 8-phase kernels, small grids with split-K; the
-# last case scales the weights by 1e-3 so that most w_lo are f16 subnormals (the MFMA must not flush them)
+# last case scales the weights by 1e-3 (unscaled, w_hi itself would be an f16 subnormal: the packing's 2^s keeps it
+# normal)
 F16X2_CONV_CASES = [(32, 64, 2, 150, 1.0), (64, 64, 2, 129, 1.0), (64, 128, 4, 64, 1.0), (128, 128, 4, 64, 1.0),
                     (128, 256, 8, 32, 1.0), (256, 512, 8, 16, 1.0), (40, 20, 2, 33, 1.0), (32, 64, 1, 20, 1.0),
                     (64, 64, 2, 96, 1e-3)]
