@@ -372,4 +372,4 @@ def test_split_encoder_first_blocks_run_f16x2(cuda):
         nv.call = orig
     assert calls[0] == ("ic2_from_rgb_conv_f16", None)
     codes = [c for n, c in calls[1:]]
-    assert len(codes) == 16 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}
+    assert len(codes) == 14 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}
