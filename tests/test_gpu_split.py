@@ -358,8 +358,9 @@ def test_split_encoder_first_blocks_run_f16x2(cuda):
     orig = nv.call
 
     def rec(name, *args):
-        if name in ("ic2_conv3x3_gn_fwd", "ic2_conv_igemm_ws", "ic2_from_rgb_conv_f16", "ic2_from_rgb_conv_x3"):
-            calls.append((name, args[3] if name in ("ic2_conv3x3_gn_fwd", "ic2_conv_igemm_ws") else None))
+        convs = ("ic2_conv3x3_gn_fwd", "ic2_conv3x3_gn_fwd_scaled", "ic2_conv_igemm_ws")
+        if name in convs + ("ic2_from_rgb_conv_f16", "ic2_from_rgb_conv_x3"):
+            calls.append((name, args[3] if name in convs else None))
         return orig(name, *args)
 
     torch.manual_seed(0)
@@ -372,4 +373,4 @@ def test_split_encoder_first_blocks_run_f16x2(cuda):
         nv.call = orig
     assert calls[0] == ("ic2_from_rgb_conv_f16", None)
     codes = [c for n, c in calls[1:]]
-    assert len(codes) == 14 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}
+    assert len(codes) == 16 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}
