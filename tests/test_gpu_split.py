@@ -351,7 +351,7 @@ def test_from_rgb_f16_out(cuda, cin, cout, n, h, w):
 
 
 def test_split_encoder_first_blocks_run_f16x2(cuda):
-    """The benched split encoder ('bf16x3') runs its first IC2_SPLIT_F16_BLOCKS = 2 blocks' convs as split-weight f16
+    """The benched split encoder ('bf16x3') runs its first IC2_SPLIT_F16_BLOCKS = 3 blocks' convs as split-weight f16
     (the f16 statistics-epilogue kernels) and the rest as split bf16."""
     import image_compression_2_amd as ic2
     calls = []
@@ -373,4 +373,4 @@ def test_split_encoder_first_blocks_run_f16x2(cuda):
         nv.call = orig
     assert calls[0] == ("ic2_from_rgb_conv_f16", None)
     codes = [c for n, c in calls[1:]]
-    assert len(codes) == 16 and codes[:4] == [nv.F16X2] * 4 and set(codes[4:]) == {nv.BF16X3}
+    assert len(codes) == 16 and codes[:6] == [nv.F16X2] * 6 and set(codes[6:]) == {nv.BF16X3}
