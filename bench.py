@@ -88,8 +88,8 @@ F32_PEAK_TFLOPS = 157.3     # f32 MFMA / VALU
 HBM_PEAK_GBS = 8000.0
 N_CODES = 256               # 8-bit codes: the record's histogram width
 
-CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gnin_gn_fwd", "ic2_from_rgb_conv",
-                "ic2_from_rgb_conv_x3", "ic2_from_rgb_conv_f16", "ic2_conv_wino")
+CONV_ENTRIES = ("ic2_conv_igemm_ws", "ic2_conv3x3_gn_fwd", "ic2_conv3x3_gn_fwd_scaled", "ic2_conv3x3_gnin_gn_fwd",
+                "ic2_from_rgb_conv", "ic2_from_rgb_conv_x3", "ic2_from_rgb_conv_f16", "ic2_conv_wino")
 TRAIN_CONV_ENTRIES = CONV_ENTRIES + ("ic2_conv_wgrad", "ic2_conv_wgrad_oihw")
 FLR_ENTRIES = ("ic2_flrelu_nhwc", "ic2_flrelu_nhwc16")
 
@@ -169,13 +169,13 @@ def conv_call_plan(nv, name, args):
     if name == "ic2_conv_igemm_ws":
         dt, odt, n, h, w, cin_p, cout_p, cv, kh, kw, pad = args[3:14]
         layout = args[23]
-    elif name == "ic2_conv3x3_gn_fwd":
+    elif name in ("ic2_conv3x3_gn_fwd", "ic2_conv3x3_gn_fwd_scaled"):
         dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[3], args[4:13]
         odt, layout = dt, nv.NHWC
         if dt == nv.BF16X3:  # split-bf16 encoder: bf16 GEMM over the tripled K, f32 out
             dt, odt = nv.BF16, nv.F32
-        elif dt == nv.F16X2:  # its first blocks: f16 GEMM over the doubled K, f32 out
-            odt = nv.F32
+        elif dt == nv.F16X2:  # its first blocks: f16 GEMM over the doubled K, f16 out
+            odt = nv.F16
     elif name == "ic2_conv3x3_gnin_gn_fwd":
         dt, (n, h, w, cin_p, cout_p, cv, kh, kw, pad) = args[5], args[6:15]
         odt, layout = dt, nv.NHWC
@@ -195,7 +195,8 @@ def conv_call_plan(nv, name, args):
         raise KeyError(name)
     ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
     plan = nv.conv_plan(dt, odt, layout, n, h, w, cin_p, cout_p, cv, kh, kw, pad)
-    if name == "ic2_conv3x3_gn_fwd" and odt == nv.F32 and plan.startswith("hg4_o"):
+    if (name in ("ic2_conv3x3_gn_fwd", "ic2_conv3x3_gn_fwd_scaled") and (odt == nv.F32 or dt == nv.F16X2)
+            and plan.startswith("hg4_o")):
         # the split conv with the GroupNorm statistics in its epilogue (igemm.hip x3_gn_hg4: 12-row tiles for 64-wide)
         f16 = plan.endswith("_f16")
         base = plan[:-4] if f16 else plan

@@ -107,9 +107,13 @@ __device__ __forceinline__ void ig_store4v(const IgemmArgs& a, int p, int nn, in
       float s_[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) s_[r] = __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
+      const h2 q0 = h2{(_Float16)s_[0], (_Float16)s_[1]}, q1 = h2{(_Float16)s_[2], (_Float16)s_[3]};
+      if (vout != nullptr) {  // the statistics of what is stored (the f16 values), as the separate pass sees them
+        (*vout)[0] = (float)q0.x; (*vout)[1] = (float)q0.y; (*vout)[2] = (float)q1.x; (*vout)[3] = (float)q1.y;
+      }
       uint2 pk;
-      pk.x = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[0], (_Float16)s_[1]});
-      pk.y = __builtin_bit_cast(uint32_t, h2{(_Float16)s_[2], (_Float16)s_[3]});
+      pk.x = __builtin_bit_cast(uint32_t, q0);
+      pk.y = __builtin_bit_cast(uint32_t, q1);
       *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.y) + e) = pk;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + e) = make_float4(v[0], v[1], v[2], v[3]);

@@ -823,8 +823,8 @@ static int conv3x3_gn_fwd_impl(const void* x, const void* w, void* y, int dtype,
                                 (stats_floats - sf) / 2, conv_ws, conv_ws_bytes, fuse, s, in_gn, in_slope, out_mul);
   if (nch == -2) return IC2_E_UNSUPPORTED;
   if (nch < 0) return IC2_E_INVALID;
-  if (nch == 0)  // split inputs: the conv wrote f32
-    return ic2_group_norm_stats(y, dtype == IC2_BF16X3 || dtype == IC2_F16X2 ? IC2_F32 : dtype, n, ho * wo, cout_p, cout_valid, groups, eps,
+  if (nch == 0)  // split inputs: the conv wrote f32 (split bf16) / f16 (split-weight f16)
+    return ic2_group_norm_stats(y, dtype == IC2_BF16X3 ? IC2_F32 : dtype == IC2_F16X2 ? IC2_F16 : dtype, n, ho * wo, cout_p, cout_valid, groups, eps,
                                 stats, stream);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n * groups)), dim3(64), 0, s, part, n * groups, nch,
                      (double)ho * wo * (cout_valid / groups), eps, stats);
@@ -933,6 +933,7 @@ extern "C" int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dty
   else if (dtype_in == IC2_F32 && dtype_out == IC2_BF16X3) IC2_GN_LAUNCH(float, bf16x3_t);
   else if (dtype_in == IC2_F32 && dtype_out == IC2_F16) IC2_GN_LAUNCH(float, _Float16);
   else if (dtype_in == IC2_F16 && dtype_out == IC2_F16) IC2_GN_LAUNCH(_Float16, _Float16);
+  else if (dtype_in == IC2_F16 && dtype_out == IC2_BF16X3) IC2_GN_LAUNCH(_Float16, bf16x3_t);
   else IC2_CHECK_ARG(false, "gn_lrelu_pool: bad dtypes");
 #undef IC2_GN_LAUNCH
   IC2_CHECK_LAUNCH("gn_lrelu_pool");

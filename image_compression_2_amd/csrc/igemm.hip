@@ -1782,7 +1782,9 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   const int ho = h + 2 * pad - kh + 1, wo = w_ + 2 * pad - kw + 1;
   const int64_t M = (int64_t)n * ho * wo;
   if (dtype == IC2_BF16X3 || dtype == IC2_F16X2) {
-    // default on: the statistics epilogue of the non-persistent hg4 costs less than the separate f32 pass saves
+    // default on: the statistics epilogue of the non-persistent hg4 costs less than the separate f32 pass saves.
+    // Output f32 (split bf16) / f16 (split-weight f16: its consumer's operand is f16 anyway)
+    const int ydt = dtype == IC2_F16X2 ? IC2_F16 : IC2_F32;
     H4Plan p;
     const bool fuse = conv_gn_fuses(dtype, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, groups, fuse_mode) &&
                       in_gn == nullptr && bias != nullptr && part != nullptr &&
@@ -1793,8 +1795,8 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
       return -2;
     }
     if (!fuse) {
-      const int rc = ic2_conv_igemm_ws(x, w, y, dtype, IC2_F32, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad,
-                                       ho, wo, nullptr, bias, 0, 0.f, 1.f, -1.f, out_mul, IC2_LAYOUT_NHWC, workspace,
+      const int rc = ic2_conv_igemm_ws(x, w, y, dtype, ydt, n, h, w_, cin_p, cout_p, cout_valid, kh, kw, pad, ho, wo,
+                                       nullptr, bias, 0, 0.f, 1.f, -1.f, out_mul, IC2_LAYOUT_NHWC, workspace,
                                        ws_bytes, s);
       return rc == IC2_OK ? 0 : -1;
     }
@@ -1804,7 +1806,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
     a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
     a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = out_mul;
-    a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = IC2_F32;
+    a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = ydt;
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;
     a.in_gn = nullptr; a.in_slope = 0.f;
@@ -1816,7 +1818,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     for (int i0 = 0; i0 < n; i0 += nc) {  // chunks of whole images (< 2^31 input bytes per launch)
       const int cnt = n - i0 < nc ? n - i0 : nc;
       a.x = reinterpret_cast<const char*>(x) + (int64_t)i0 * h * w_ * a.x_pix * 2;
-      a.y = reinterpret_cast<char*>(y) + (int64_t)i0 * ho * wo * cout_p * 4;
+      a.y = reinterpret_cast<char*>(y) + (int64_t)i0 * ho * wo * cout_p * (ydt == IC2_F16 ? 2 : 4);
       a.gn_part = part + (int64_t)i0 * groups * ntile * 2;
       a.n = cnt;
       a.M = (int)((int64_t)cnt * ho * wo);

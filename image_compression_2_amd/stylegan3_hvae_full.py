@@ -189,11 +189,13 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     wp, bp = _packed(conv, x, dt, cache, stream)
     cout_p = wp.shape[0]
     ho, wo = x.h + 2 * pad - kh + 1, x.w + 2 * pad - kw + 1
+    # split-weight f16: the conv output stored f16 (its consumer, the f16 GroupNorm output, rounds there anyway)
+    ydt = torch.float16 if x.h2 else torch.float32
     if x.split and bool(nv.query("ic2_conv3x3_gn_fuses", x.code, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw, pad,
                                  norm.num_groups, int(fuse))):
-        # split bf16 / split-weight f16, 64- / 128-wide layers: the 4-wave halo GEMM writes f32 and the statistics in
-        # one launch
-        y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
+        # split bf16 / split-weight f16, 64- / 128-wide layers: the 4-wave halo GEMM writes the output and the
+        # statistics in one launch
+        y = torch.empty([x.n, ho, wo, cout_p], dtype=ydt, device=x.t.device)
         nfl = int(nv.query("ic2_conv3x3_gn_stats_floats", x.code, x.n, x.h, x.w, x.k_p, cout_p, kh, kw, pad,
                            norm.num_groups))
         stats = torch.empty([nfl], dtype=torch.float32, device=x.t.device)
@@ -210,16 +212,16 @@ def _conv_gn(conv: nn.Conv2d, norm: nn.GroupNorm, x: _Act, dt, cache: dict, stre
     if x.split:
         # split bf16: one bf16 implicit GEMM over the tripled K (its input [hi | lo] read as [hi | hi | lo]), f32 out,
         # GroupNorm statistics on the f32 values (split-weight f16: the f16 GEMM over the doubled K)
-        y = torch.empty([x.n, ho, wo, cout_p], dtype=torch.float32, device=x.t.device)
+        y = torch.empty([x.n, ho, wo, cout_p], dtype=ydt, device=x.t.device)
         nv.note_flops(_conv_flops(x.n, ho, wo, cout, cin, kh, kw))
-        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, nv.F32, x.n, x.h, x.w, x.k_p, cout_p, cout, kh, kw,
-                      pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, _out_mul(conv, cache), nv.NHWC, stream,
-                      x.t.device)
+        nv.conv_igemm(nv.ptr(x.t), nv.ptr(wp), nv.ptr(y), x.code, nv.dtype_code(ydt), x.n, x.h, x.w, x.k_p, cout_p,
+                      cout, kh, kw, pad, ho, wo, None, nv.ptr(bp), 0, 0.0, 1.0, -1.0, _out_mul(conv, cache), nv.NHWC,
+                      stream, x.t.device)
         ya = _Act(y, cout)
         nfl = int(nv.query("ic2_group_norm_stats_floats", ya.n, ya.h * ya.w, norm.num_groups))
         stats = torch.empty([nfl], dtype=torch.float32, device=y.device)
-        nv.call("ic2_group_norm_stats", nv.ptr(y), nv.F32, ya.n, ya.h * ya.w, ya.c_p, ya.c, norm.num_groups,
-                float(norm.eps), nv.ptr(stats), stream)
+        nv.call("ic2_group_norm_stats", nv.ptr(y), nv.dtype_code(ydt), ya.n, ya.h * ya.w, ya.c_p, ya.c,
+                norm.num_groups, float(norm.eps), nv.ptr(stats), stream)
         return ya, stats
     if dt == torch.float16:
         # f16 (the training precision's inference forward): the conv, then the separate statistics pass (the fused

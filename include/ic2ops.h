@@ -275,8 +275,8 @@ int ic2_group_norm_stats(const void* y, int dtype, int n, int hw, int c_p, int c
 
 /* GroupNorm apply + F.leaky_relu(0.2) (+ AvgPool2d(2,2) when pool != 0), VGGBlock.forward :183-191:
  *   out = pool(lrelu((y - mean) * rstd * gamma[c] + beta[c]))  NHWC -> NHWC (floor pooling).  dtype_out may be
- *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][2 * c_p]); dtype_in IC2_F32 -> dtype_out IC2_F16 is the
- *   input of an IC2_F16X2 conv. */
+ *   IC2_BF16X3 (f32 arithmetic, then split: out [n][oh][ow][2 * c_p]), also from dtype_in IC2_F16 (an IC2_F16X2
+ *   conv's output); dtype_out IC2_F16 is the input of an IC2_F16X2 conv. */
 int ic2_gn_lrelu_pool(const void* y, void* out, int dtype_in, int dtype_out, int n, int h, int w, int c_p, int c,
                       int groups, const float* stats, const float* gamma, const float* beta, float slope,
                       int pool, void* stream);
@@ -367,7 +367,8 @@ int ic2_gap_bwd(const float* dpooled, void* dx, int dtype, int n, int hw, int c_
  * [hi | lo] with cin_p = the tripled (GEMM K) channel count, w from ic2_pack_weight(IC2_BF16X3), y f32 NHWC; the
  * statistics come out of the 4-wave halo GEMM's epilogue (on the f32 values as stored) when it runs a 64- / 128-wide
  * layer with 32 groups (fuse != 0), else the separate pass.  dtype IC2_F16X2: the same with the f16 input and
- * [hi | lo] f16 weights (cin_p = the doubled K), the f16 instances of those kernels. */
+ * [hi | lo] f16 weights (cin_p = the doubled K), the f16 instances of those kernels, y f16 NHWC (the statistics of
+ * the stored f16 values). */
 int64_t ic2_conv3x3_gn_stats_floats(int dtype, int n, int h, int w, int cin_p, int cout_p, int kh, int kw, int pad,
                                     int groups);
 int ic2_conv3x3_gn_fwd(const void* x, const void* w, void* y, int dtype, int n, int h, int w_, int cin_p, int cout_p,

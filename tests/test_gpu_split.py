@@ -247,9 +247,9 @@ F16X2_CONV_CASES = [(32, 64, 2, 150, 1.0), (64, 64, 2, 129, 1.0), (64, 128, 4, 6
 
 @pytest.mark.parametrize("cin,cout,n,size,wscale", F16X2_CONV_CASES)
 def test_f16x2_conv_gn_matches_fp64(cuda, cin, cout, n, size, wscale):
-    """_conv_gn on an f16 activation (IC2_F16X2): the f32 output within 1e-5 (relative to max |y|) of F.conv2d in
-    fp64 on the f16-rounded activation and the unrounded weights (the weight split carries ~22 bits), and the
-    GroupNorm statistics of that output."""
+    """_conv_gn on an f16 activation (IC2_F16X2): the f16 output within its rounding (2^-11 relative) plus 1e-5 of
+    max |y| of F.conv2d in fp64 on the f16-rounded activation and the unrounded weights (the weight split carries ~22
+    bits; before the output rounding the conv is within 1e-5), and the GroupNorm statistics of that output."""
     g = torch.Generator().manual_seed(cin * 5 + cout + size)
     conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
     with torch.no_grad():
@@ -261,28 +261,28 @@ def test_f16x2_conv_gn_matches_fp64(cuda, cin, cout, n, size, wscale):
     plan = nv.conv_plan(nv.F16X2, nv.F32, nv.NHWC, n, size, size, a.k_p, nv.pad32(cout), cout, 3, 3, 1)
     y, st = shf._conv_gn(conv.to(cuda), norm.to(cuda), a, torch.bfloat16, {}, nv.stream_of())
     torch.cuda.synchronize()
-    assert y.t.dtype == torch.float32 and not y.split
+    assert y.t.dtype == torch.float16 and not y.split
     r = F.conv2d(x.to(torch.float16).double(), conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(),
                  padding=1)
     got = y.t[..., :cout].cpu().double().permute(0, 3, 1, 2)
-    err = (got - r).abs().max().item() / r.abs().max().item()
-    print(f"[f16x2 conv {cin}->{cout} n{n} {size}^2 w*{wscale:g} plan {plan}] max rel err {err:.2e}")
-    assert err < 1e-5
+    ex = ((got - r).abs() - 2 ** -11 * r.abs()).max().item() / r.abs().max().item()
+    print(f"[f16x2 conv {cin}->{cout} n{n} {size}^2 w*{wscale:g} plan {plan}] max err beyond f16 rounding {ex:.2e}")
+    assert ex < 1e-5
     assert (y.t[..., cout:] == 0).all()
     groups = norm.num_groups
     rg = r.reshape(n, groups, -1)
     mean, var = rg.mean(-1), rg.var(-1, unbiased=False)
     s = st[: n * groups * 2].view(n, groups, 2).cpu().double()
-    assert torch.allclose(s[..., 0], mean, rtol=1e-4, atol=1e-5 * r.abs().max().item())
-    assert torch.allclose(s[..., 1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+    assert torch.allclose(s[..., 0], mean, rtol=1e-4, atol=1e-4 * r.abs().max().item())
+    assert torch.allclose(s[..., 1], 1 / torch.sqrt(var + 1e-5), rtol=2e-4)
 
 
 @pytest.mark.parametrize("cin,cout,n,h,w", [(32, 64, 8, 126, 124), (64, 128, 8, 126, 124), (64, 64, 8, 1024, 1024),
                                              (64, 128, 8, 512, 512)])
 def test_f16x2_conv_gn_fused_epilogue(cuda, cin, cout, n, h, w):
-    """The f16 instances of the statistics-epilogue halo GEMMs (hg4_*_gn_kernel_f16): the same f32 output bits as
-    the unfused call and statistics within 1e-6 of the separate pass, on ragged tiles and on the C4 block-0 / block-1
-    conv2 shapes."""
+    """The f16 instances of the statistics-epilogue halo GEMMs (hg4_*_gn_kernel_f16): the same f16 output bits as
+    the unfused call and statistics (of the stored f16 values) within 1e-6 of the separate pass, on ragged tiles and
+    on the C4 block-0 / block-1 conv2 shapes."""
     g = torch.Generator().manual_seed(cin + cout + h + 1)
     conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
     with torch.no_grad():

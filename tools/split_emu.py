@@ -26,10 +26,10 @@ CONV_IDX = [0]
 
 def make_conv(mode):
     base = mode
-    if mode.startswith('mix') or mode.startswith('tail') or mode.startswith('hmix'):
+    if mode.startswith('mix') or mode.startswith('tail') or mode.startswith('hmix') or mode.startswith('hy'):
         # mixK: the first K convs (from_rgb = 0, block i conv1 = 1 + 2i, conv2 = 2 + 2i) in bf16, the rest split;
         # tailK: the convs from index K on in bf16, the ones before split
-        k = int(mode[4:] if mode.startswith('hmix') else mode[3:] if mode.startswith('mix') else mode[4:])
+        k = int(mode[4:] if mode.startswith('hmix') else mode[2:] if mode.startswith('hy') else mode[3:] if mode.startswith('mix') else mode[4:])
     def conv(x, w, b):
         mode = base
         if base.startswith('mix'):
@@ -37,6 +37,10 @@ def make_conv(mode):
             CONV_IDX[0] += 1
         elif base.startswith('hmix'):
             mode = 'w2_f16' if 0 < CONV_IDX[0] < k else 'split_bf16'
+            CONV_IDX[0] += 1
+        elif base.startswith('hy'):  # hmixK with those convs' outputs stored f16 as well
+            mode = 'w2_f16' if 0 < CONV_IDX[0] < k else 'split_bf16'
+            y16 = 0 < CONV_IDX[0] < k
             CONV_IDX[0] += 1
         elif base.startswith('tail'):
             mode = 'bf16' if CONV_IDX[0] >= k else 'split_bf16'
@@ -57,6 +61,8 @@ def make_conv(mode):
             if mode.endswith('4'):
                 y = y + F.conv2d(xl, wl, None, padding=1)
         y = y.float()
+        if base.startswith('hy') and y16:
+            y = y.half().float()
         if mode in ('bf16',):
             y = y.to(torch.bfloat16).float()
         return y
@@ -69,8 +75,8 @@ def enc_forward(mode):
     if mode.startswith('mix'):  # activations stored bf16 while the convs consuming them are bf16
         k = int(mode[3:])
         store = lambda t: t.to(torch.bfloat16).float() if CONV_IDX[0] < k else t
-    if mode.startswith('hmix'):  # convs 1 .. K-1 (block 0 = 1, 2) x f16, w split f16; their inputs stored f16
-        k = int(mode[4:])
+    if mode.startswith('hmix') or mode.startswith('hy'):  # convs 1 .. K-1 (block 0 = 1, 2) x f16, w split f16; their inputs stored f16
+        k = int(mode[4:] if mode.startswith('hmix') else mode[2:])
         store = lambda t: t.to(torch.float16).float() if 0 < CONV_IDX[0] < k else t
     if mode.startswith('tail'):
         k = int(mode[4:])
