@@ -122,7 +122,8 @@ _FROM_RGB_DIRECT = nv.knob("IC2_FROM_RGB_DIRECT", 1) != 0
 # knob IC2_SPLIT_F16_BLOCKS: in the split ('bf16x3') mode the first K blocks' convs take f16 activations against
 # split f16 weights (IC2_F16X2, two f16 MFMAs per product instead of three bf16 ones): K = 3 (blocks 0-2,
 # the 1024^2 .. 256^2 levels at C4) by default, 0 = every conv split bf16.  Measured (profiles/r5_split_f16_blocks.txt):
-# K 0 / 2 / 3 -> C4 316 / 340 / 346 img/s, C2 1426 / 1451 / 1461, C2 index mismatches 18 / 37 / 34 of 262144
+# K 0 / 2 / 3 -> C4 316 / 340 / 346 img/s, C2 1426 / 1451 / 1461 (f32 conv outputs), C2 index mismatches 18 / 37 / 34
+# of 262144; with f16 conv outputs (default) K = 3 -> C4 371-378, C2 1482-1520, 63 mismatches
 _SPLIT_F16_BLOCKS = nv.knob("IC2_SPLIT_F16_BLOCKS", 3)
 # knob IC2_GN_IN_FUSE=1 applies norm1 + lrelu inside conv2's halo-conv staging instead of materialising it.  Bit-identical
 # but measured level on MI355X (C2 1438.0 -> 1439.4, C4 415.5 -> 415.9 img/s, same box: the saved pass is paid back in
