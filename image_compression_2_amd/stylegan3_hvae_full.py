@@ -103,7 +103,9 @@ def _conv_flops(n, ho, wo, cout, cin, kh, kw):
 
 
 def _conv(conv: nn.Conv2d, x: _Act, dt, cache: dict, stream):
-    """nn.Conv2d (3x3 or k x k, stride 1, 'same' padding) + bias on MFMA."""
+    """nn.Conv2d (3x3 or k x k, stride 1, 'same' padding) + bias on MFMA (plain activations; the split ones go through
+    _conv_gn)."""
+    assert not x.split, "split activations are consumed by _conv_gn"
     cout, cin, kh, kw = conv.weight.shape
     pad = conv.padding[0]
     wp, bp = _packed(conv, x, dt, cache, stream)
