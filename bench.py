@@ -237,19 +237,28 @@ def training_flops_per_image(enc, G, res):
     return 2 * e + (e - rgb) + e + 2 * s_mod
 
 
+def _h2_blocks(enc_split):
+    """Encoder blocks whose convs run split-weight f16 in the split mode (stylegan3_hvae_full._SPLIT_F16_BLOCKS)."""
+    from image_compression_2_amd import stylegan3_hvae_full as shf
+    return shf._SPLIT_F16_BLOCKS if enc_split else 0
+
+
 def algorithmic_bytes_per_image(enc, G, res, esz, enc_split=False):
     """Compulsory HBM bytes of the conv launches per image: each conv reads its input activation and writes
     its output once (padded channel strides, esz bytes each; ToRGB writes 3 f32 channels).  enc_split: the
     split-bf16 encoder ('bf16x3') reads its conv operands as [hi | lo] bf16 (4 B per channel; the GEMM reads the hi
-    block twice, the second time from cache) and writes f32 (4 B); from_rgb writes the split form.  Weights are per
-    launch, not per image, and are added by the caller."""
+    block twice, the second time from cache) and writes f32 (4 B); its first blocks in split-weight f16 read and write
+    f16 (2 B), and from_rgb writes f16 when block 0 is one of them, else the split form.  Weights are per launch, not
+    per image, and are added by the caller."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
-    e_in, e_out = (4, 4) if enc_split else (esz, esz)
+    nh2 = _h2_blocks(enc_split)
     total, h = 0.0, res
-    total += h * h * (enc.from_rgb.in_channels * 4 + p32(enc.from_rgb.out_channels) * (4 if enc_split else esz))
-    for blk in enc.blocks:
+    total += h * h * (enc.from_rgb.in_channels * 4 +
+                      p32(enc.from_rgb.out_channels) * ((2 if nh2 > 0 else 4) if enc_split else esz))
+    for i, blk in enumerate(enc.blocks):
         if h <= 1:
             break
+        e_in, e_out = ((2, 2) if i < nh2 else (4, 4)) if enc_split else (esz, esz)
         ci, co = p32(blk.conv1.in_channels), p32(blk.conv1.out_channels)
         total += h * h * (ci * e_in + co * e_out) + h * h * (co * e_in + co * e_out)
         h = h // 2
@@ -265,16 +274,19 @@ def algorithmic_bytes_per_image(enc, G, res, esz, enc_split=False):
 
 def weight_bytes(enc, G, res, esz, enc_split=False):
     """Packed weight bytes of the convs one step runs, and their count (= conv calls per step).  enc_split: the
-    encoder's packed weights are [hi | lo | hi] (3 bf16 per value)."""
+    encoder's packed weights are [hi | lo | hi] (3 bf16 per value), [hi | lo] f16 (2 per value) in its split-weight
+    f16 blocks."""
     p32 = lambda c: (int(c) + 31) // 32 * 32
-    convs, h = [enc.from_rgb], res
-    for blk in enc.blocks:
+    nh2 = _h2_blocks(enc_split)
+    convs, h = [(enc.from_rgb, 6)], res
+    for i, blk in enumerate(enc.blocks):
         if h <= 1:
             break
-        convs += [blk.conv1, blk.conv2]
+        ew = 4 if i < nh2 else 6
+        convs += [(blk.conv1, ew), (blk.conv2, ew)]
         h = h // 2
-    ew = 6 if enc_split else esz
-    tot = sum(p32(c.out_channels) * p32(c.in_channels) * c.kernel_size[0] * c.kernel_size[1] * ew for c in convs)
+    tot = sum(p32(c.out_channels) * p32(c.in_channels) * c.kernel_size[0] * c.kernel_size[1] * (ew if enc_split else esz)
+              for c, ew in convs)
     C = p32(G.synthesis.input.channels)
     tot += C * C * esz
     tot += sum(p32(L.out_channels) * p32(L.in_channels) * L.conv_kernel ** 2 * esz for L in G.synthesis.layers())
