@@ -568,6 +568,7 @@ template <int COUT, bool X3 = false, bool H16 = false>
 __global__ void __launch_bounds__(256) from_rgb_kernel(const float* __restrict__ x, int cin, const void* __restrict__ wp,
                                                        int cin_p, const float* __restrict__ bias, bf16_t* __restrict__ y,
                                                        int h, int w, int tiles_x, int tiles_y) {
+  static_assert(X3 || !H16, "the f16 output is the f32-weight (X3) kernel's");
   constexpr int TH = 8, TW = 32, HH = TH + 2, HW = TW + 2;
   __shared__ float xin[4][HH][HW + 1];
   __shared__ __attribute__((aligned(16))) float wl[36][COUT];  // [tap * cin + c][o]
