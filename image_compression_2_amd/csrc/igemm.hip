@@ -631,14 +631,22 @@ __device__ __forceinline__ int h4_off(int row, int chunk) { return row * 64 + ((
 #ifndef IC2_HG4_ABL
 #define IC2_HG4_ABL 0
 #endif
+// IC2_HG4_PAIR=0 (diagnostic builds): the split-weight f16 statistics-epilogue kernels in the plain K order
+#ifndef IC2_HG4_PAIR
+#define IC2_HG4_PAIR 1
+#endif
 
 // HB: the next block's halo is issued as one burst at the block's first tap, every wave exactly HPW DMAs (the ones
 // past the halo into a 1-KiB dummy slot), so no per-tap selection of a halo-offset register (a uniform branch
 // chain, ~60 SALU per step) and a wait count that depends only on the tap
+// PAIR (split-weight f16 input, IC2_F16X2, TPB = 2): K blocks cb and cb + CB/2 (x * w_hi, x * w_lo) read the same
+// stored channel block, so the steps run tap-major over the pair -- (tap, hi), (tap, lo) share one barrier step and one
+// set of halo fragments, and each stored block's halo is loaded once for its 18 steps instead of twice for 9 each
 template <int I, int J, int WGO, int WGP, int TW, int NS, bool HB = false, bool F16 = false, int TPB = 1,
-          bool GN = false>
+          bool GN = false, bool PAIR = false>
 __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int tiles_y) {
   using G = H4<I, J, WGO, WGP, TW, NS, HB>;
+  static_assert(!PAIR || (TPB == 2 && HB), "PAIR: two taps per barrier step with the halo burst");
   static_assert((G::BO / 16) % 4 == 0 || (TPB == 2 && NS == 4), "uneven weight DMAs need the L = 1 multi-tap loop");
   constexpr int LA = NS - 1;  // weight slabs in flight ahead of the step being computed
   constexpr int NWI = G::NWI, HPW = G::HPW;
@@ -693,9 +701,25 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
   const bool live = o0 + obase < a.cout_p;
   const int CB = a.cin_p >> 5;
   const int nq = CB * 9;
+  constexpr int SPB = PAIR ? 18 : 9;    // K-steps per halo block
+  const int HBK = PAIR ? CB >> 1 : CB;  // halo blocks
+  // K-step t -> (halo block, K block, tap)
+  auto step_of = [&](int t, int& hbk, int& cb, int& tap) {
+    if constexpr (PAIR) {
+      hbk = t / 18;
+      const int r = t - hbk * 18;
+      tap = r >> 1;
+      cb = hbk + (r & 1) * (CB >> 1);
+    } else {
+      cb = t / 9;
+      tap = t - cb * 9;
+      hbk = cb;
+    }
+  };
 
   auto issue_w = [&](int t) {  // weight slab of K-step t -> slab t % NS
-    const int cb = t / 9, tap = t - (t / 9) * 9;
+    int hbk_, cb, tap;
+    step_of(t, hbk_, cb, tap);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(wg + ((int64_t)tap * a.cin_p + cb * 32) * 2), 0, t < nq ? kOob : 0, kRsrcWord3);
     char* dst = wsl + (t % NS) * G::WS_B;
@@ -739,8 +763,8 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
     constexpr int L = NS / TPB - 1;
     const int nst = (nq + TPB - 1) / TPB;
     auto burst_at = [&](int st) {  // block cb0+1's halo: first step with no tap of block cb0-1
-      const int t0 = TPB * st, cb0 = t0 / 9;
-      return t0 - cb0 * 9 < TPB && cb0 + 1 < CB;
+      const int t0 = TPB * st, cb0 = t0 / SPB;
+      return t0 - cb0 * SPB < TPB && cb0 + 1 < HBK;
     };
 #pragma unroll
     for (int t = 0; t < TPB * L; ++t) issue_w(t);
@@ -755,18 +779,22 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
         for (int u = 0; u < TPB; ++u) issue_w(t0 + u + TPB * L);
       }
       const bool burst = burst_at(s);  // first read >= 3 steps later
-      if (burst) issue_hb(t0 / 9 + 1);
+      if (burst) issue_hb(t0 / SPB + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < TPB; ++u) {
         if ((IC2_HG4_ABL & 4) && s > 0) break;
-        const int t = t0 + u, cb = t / 9, tap = t - cb * 9;
+        const int t = t0 + u;
+        int hbk, cb, tap;
+        step_of(t, hbk, cb, tap);
         // the swizzle depends on the absolute halo row: the tap shift goes into the row, not the base pointer
         const int sh = (tap / 3) * G::HW + tap % 3;
-        const char* hb = hal + (cb & 1) * G::HALO_B;
+        const char* hb = hal + (hbk & 1) * G::HALO_B;
         const char* wl = wsl + (t % NS) * G::WS_B;
+        if (!PAIR || u == 0) {  // PAIR: the step's second K block reads the same halo fragments
 #pragma unroll
-        for (int j = 0; j < J; ++j) bfr[u][j] = *reinterpret_cast<const bf16x8*>(hb + h4_off(brow[j] + sh, fh));
+          for (int j = 0; j < J; ++j) bfr[u][j] = *reinterpret_cast<const bf16x8*>(hb + h4_off(brow[j] + sh, fh));
+        }
 #pragma unroll
         for (int i = 0; i < I; ++i) af[u][i] = *reinterpret_cast<const bf16x8*>(wl + h4_off(obase + i * 16 + fr, fh));
       }
@@ -780,8 +808,8 @@ __device__ __forceinline__ void hg4_body(const IgemmArgs& a, int tiles_x, int ti
             for (int i = 0; i < I; ++i)
 #pragma unroll
               for (int j = 0; j < J; ++j) {
-                if constexpr (IC2_HG4_ABL & 8) asm volatile("" ::"v"(af[u][i]), "v"(bfr[u][j]));
-                else acc[i][j] = mfma32<F16>(af[u][i], bfr[u][j], acc[i][j]);
+                if constexpr (IC2_HG4_ABL & 8) asm volatile("" ::"v"(af[u][i]), "v"(bfr[PAIR ? 0 : u][j]));
+                else acc[i][j] = mfma32<F16>(af[u][i], bfr[PAIR ? 0 : u][j], acc[i][j]);
               }
           }
         }
@@ -973,18 +1001,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 hg4_o64_w32_t12_gn_kernel(IgemmArgs a, int tx, int ty) {
   hg4_body<4, 6, 1, 4, 32, 4, true, false, 2, true>(a, tx, ty);
 }
-// the same three with f16 operands: the split encoder's first blocks (IC2_F16X2: f16 input, [hi | lo] f16 weights)
+// the same three with f16 operands: the split encoder's first blocks (IC2_F16X2: f16 input, [hi | lo] f16 weights),
+// the two-tap-per-step ones walking each tap's hi / lo K blocks as one step (PAIR)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 hg4_o64_w32_p3_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
   hg4_body<4, 4, 1, 4, 32, 6, true, true, 3, true>(a, tx, ty);
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 hg4_o128_w32_p2_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
-  hg4_body<8, 4, 1, 4, 32, 4, true, true, 2, true>(a, tx, ty);
+  hg4_body<8, 4, 1, 4, 32, 4, true, true, 2, true, IC2_HG4_PAIR>(a, tx, ty);
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 hg4_o64_w32_t12_gn_kernel_f16(IgemmArgs a, int tx, int ty) {
-  hg4_body<4, 6, 1, 4, 32, 4, true, true, 2, true>(a, tx, ty);
+  hg4_body<4, 6, 1, 4, 32, 4, true, true, 2, true, IC2_HG4_PAIR>(a, tx, ty);
 }
 #undef IC2_HG4_KERNEL
 #undef IC2_HG4_KERNEL_P

@@ -280,9 +280,9 @@ def test_f16x2_conv_gn_matches_fp64(cuda, cin, cout, n, size, wscale):
 @pytest.mark.parametrize("cin,cout,n,h,w", [(32, 64, 8, 126, 124), (64, 128, 8, 126, 124), (64, 64, 8, 1024, 1024),
                                              (64, 128, 8, 512, 512)])
 def test_f16x2_conv_gn_fused_epilogue(cuda, cin, cout, n, h, w):
-    """The f16 instances of the statistics-epilogue halo GEMMs (hg4_*_gn_kernel_f16): the same f16 output bits as
-    the unfused call and statistics (of the stored f16 values) within 1e-6 of the separate pass, on ragged tiles and
-    on the C4 block-0 / block-1 conv2 shapes."""
+    """The f16 instances of the statistics-epilogue halo GEMMs (hg4_*_gn_kernel_f16, tap-major hi / lo pairs): the
+    unfused call's f16 output to an ulp, fp64 on a corner, statistics (of the stored f16 values) within 1e-5 of the
+    separate pass, on ragged tiles and on the C4 block-0 / block-1 conv2 shapes."""
     g = torch.Generator().manual_seed(cin + cout + h + 1)
     conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
     with torch.no_grad():
@@ -298,15 +298,25 @@ def test_f16x2_conv_gn_fused_epilogue(cuda, cin, cout, n, h, w):
     yf, sf = shf._conv_gn(conv, norm, a, torch.bfloat16, {}, nv.stream_of(), fuse=-1)
     yu, su = shf._conv_gn(conv, norm, a, torch.bfloat16, {}, nv.stream_of(), fuse=0)
     torch.cuda.synchronize()
-    assert torch.equal(yf.t, yu.t)
+    # the fused kernels walk each tap's hi / lo K blocks together (hg4 PAIR), the unfused ones all hi then all lo:
+    # the f32 sums differ in order, so the f16 outputs agree to an ulp
+    d = (yf.t.float() - yu.t.float()).abs()
+    assert (d <= 2 ** -10 * yu.t.float().abs() + 1e-6).all()
+    # and the fused output against fp64 on image 0's top-left 64 x 64 (windows inside the 66 x 66 crop)
+    xc = a.t[0, :66, :66, :cin].permute(2, 0, 1)[None].double().cpu()
+    r = F.conv2d(xc, conv.weight.detach().cpu().double(), conv.bias.detach().cpu().double(), padding=1)[..., :64, :64]
+    got = yf.t[0, :64, :64, :cout].permute(2, 0, 1)[None].double().cpu()
+    ex = ((got - r).abs() - 2 ** -11 * r.abs()).max().item() / r.abs().max().item()
+    assert ex < 1e-5
     del yf
     k = n * 32 * 2
     sfd, sud = sf[:k].view(n, 32, 2).double(), su[:k].view(n, 32, 2).double()
     scale = yu.t.abs().max().item()
     d_mean = (sfd[..., 0] - sud[..., 0]).abs().max().item() / scale
     d_rstd = ((sfd[..., 1] - sud[..., 1]) / sud[..., 1]).abs().max().item()
-    print(f"[f16x2 conv+GN fused {cin}->{cout} n{n} {h}x{w}] mean {d_mean:.2e} (of max|y|) rstd {d_rstd:.2e} rel")
-    assert d_mean < 1e-6 and d_rstd < 1e-6
+    print(f"[f16x2 conv+GN fused {cin}->{cout} n{n} {h}x{w}] vs fp64 {ex:.2e}; mean {d_mean:.2e} (of max|y|) "
+          f"rstd {d_rstd:.2e} rel")
+    assert d_mean < 1e-5 and d_rstd < 1e-5
 
 
 @pytest.mark.parametrize("pool", [False, True])
