@@ -486,7 +486,7 @@ static WxTile wx_tile(int n, int ho, int wo, int cout_p) {
         t.blocks = (int64_t)n * t.tx * t.ty * t.to;
         const int64_t rounds = ceil_div(t.blocks, 256);
         // ties: the fewest workgroups, then full 16-pair blocks (16 x 8 beat 15 x 8 at equal counts by 0.4-1.3 % on
-        // the SG3-T-256 148-px layers, tools/gpu_wxtile.sh)
+        // the SG3-T-256 148-px layers, profiles/r5_wino_tile_sweep.txt)
         const bool full = twp % 16 == 0, best_full = best.twp % 16 == 0;
         if (best_rounds < 0 || rounds < best_rounds ||
             (rounds == best_rounds && (t.blocks < best.blocks || (t.blocks == best.blocks && full && !best_full)))) {

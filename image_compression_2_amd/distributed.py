@@ -161,14 +161,22 @@ def allreduce_gradients(params, world=None, bucket_bytes=64 << 20):
 
 class GradReducer:
     """The gradient average of ``allreduce_gradients``, overlapped with backward: every parameter gets a
-    post-accumulate-grad hook; a bucket (parameters in reverse registration order -- the order backward produces
-    their gradients -- packed to about ``bucket_bytes``) is flattened and its all_reduce(SUM) launched
-    asynchronously (RCCL runs it on its own stream behind the flatten) as soon as its last gradient is accumulated,
-    while backward continues with the layers below.  Buckets launch strictly in index order (a completed bucket
-    waits for the ones before it), so every rank issues the same collective sequence.  ``finish()`` waits for the
-    handles, writes the averages back into .grad, and reduces what no hook covered: parameters created after the
-    reducer (the reference's per-call fc1, stylegan3_hvae_full.py:225-230) and buckets with a parameter that got no
-    gradient this step (the same on every rank: one module graph).
+    post-accumulate-grad hook; a bucket (parameters packed to about ``bucket_bytes`` in the order backward produces
+    their gradients) is flattened and its all_reduce(SUM) launched asynchronously (RCCL runs it on its own stream
+    behind the flatten) as soon as its last gradient is accumulated, while backward continues with the layers below.
+    Buckets launch strictly in index order (a completed bucket waits for the ones before it), so every rank issues
+    the same collective sequence.  ``finish()`` waits for the handles, writes the averages back into .grad, and
+    reduces what no hook covered: parameters created after the reducer (the reference's per-call fc1,
+    stylegan3_hvae_full.py:225-230) and buckets with a parameter that got no gradient this step (the same on every
+    rank: one module graph).
+
+    Bucket order.  The first step's buckets follow reverse registration order.  That order is wrong for the
+    reference's C5 encoder (img_resolution=1024 on 256^2 input): the 1x1 break (stylegan3_hvae_full.py:129-131)
+    skips blocks 8-9, whose parameters register last, get no gradient, and would hold bucket 0 -- and with it every
+    later bucket -- back until finish().  So the first step records the order the hooks actually fired in; rank 0's
+    record is broadcast (every rank then buckets identically, as DDP's rebuild_buckets) and the buckets are rebuilt
+    from it, leaving out the parameters that got no gradient.  From the second step on every bucket launches during
+    backward.  A parameter left out that later does get a gradient is reduced by finish()'s leftover pass.
 
     Usage per step: ``r.start(); loss.backward(); r.finish()``.  Autograd sums every use of a parameter before its
     AccumulateGrad node runs, so a hook fires once per backward even with the training step's two encoder passes."""
@@ -176,13 +184,25 @@ class GradReducer:
     def __init__(self, module, world=None, bucket_bytes=25 << 20):
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         self.params = [p for p in module.parameters() if p.requires_grad]
+        self.index = {id(p): i for i, p in enumerate(self.params)}
         self.module = module
+        self.bucket_bytes = bucket_bytes
+        self.rebuilt = False
+        self._fired = []
+        self._set_buckets(list(reversed(self.params)))
+        self.active = False
+        self._handles = []
+        if self.world > 1:
+            for p in self.params:
+                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _set_buckets(self, order):
         self.buckets = []
         cur, size = [], 0
-        for p in reversed(self.params):
+        for p in order:
             cur.append(p)
             size += p.numel() * 4
-            if size >= bucket_bytes:
+            if size >= self.bucket_bytes:
                 self.buckets.append(cur)
                 cur, size = [], 0
         if cur:
@@ -191,11 +211,22 @@ class GradReducer:
         for bi, b in enumerate(self.buckets):
             for p in b:
                 self.slot[id(p)] = bi
-        self.active = False
-        self._handles = []
-        if self.world > 1:
-            for p in self.params:
-                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _rebuild(self):
+        """Buckets from the recorded hook order, rank 0's copy broadcast (a collective every rank issues once, after
+        the first step's reductions)."""
+        n = len(self.params)
+        rec = torch.full((n + 1,), -1, dtype=torch.int64)
+        rec[0] = len(self._fired)
+        rec[1:1 + len(self._fired)] = torch.tensor(self._fired, dtype=torch.int64)
+        if dist.is_available() and dist.is_initialized():
+            dev = self.params[0].device if self.params and dist.get_backend() == "nccl" else torch.device("cpu")
+            t = rec.to(dev)
+            dist.broadcast(t, 0)
+            rec = t.cpu()
+        k = int(rec[0])
+        self._set_buckets([self.params[i] for i in rec[1:1 + k].tolist()])
+        self.rebuilt = True
 
     def remove(self):
         for h in self._handles:
@@ -223,6 +254,10 @@ class GradReducer:
     def _hook(self, p):
         if not self.active:
             return
+        if not self.rebuilt:
+            i = self.index.get(id(p))
+            if i is not None:
+                self._fired.append(i)
         bi = self.slot.get(id(p))
         if bi is None:
             return
@@ -257,6 +292,8 @@ class GradReducer:
         done = {id(p) for bi, b in enumerate(self.live) if self.work[bi] is not None for p in b}
         rest = [p for p in self.module.parameters() if p.grad is not None and id(p) not in done]
         n += allreduce_gradients(rest, self.world)
+        if not self.rebuilt:
+            self._rebuild()
         self.flat = [None] * len(self.buckets)
         self.work = [None] * len(self.buckets)
         return n

@@ -49,6 +49,8 @@ SNR_FLOOR_SYN = 38.0    # dB, bf16 synthesis vs the fp32 reference on identical 
 SNR_FLOOR_E2E = 38.0    # dB, benched encode + quantize + synthesis vs the reference reconstruction
 PSNR_TOL = 0.005        # dB at the 34 dB operating point, end to end (north star: 0.01)
 PSNR_TOL_46 = 0.01      # dB at 46 dB
+IDX_COUNT_BENCH = 69    # index mismatches of the benched mode at round 5 (BENCH_r05 parity): a ceiling, not a target
+IDX_COUNT_FP32 = 16     # the fp32 parity mode's count on this batch
 SNR_FLOOR_F16 = 52.0    # dB, the f16 synthesis (bench --precision f16) vs the fp32 reference (CPU emulation: 60.5)
 
 
@@ -81,6 +83,9 @@ def c2(cuda):
         enc.set_precision("bf16")
         torch.manual_seed(5)
         _, m_allbf16, _ = enc(x.to(cuda))
+        enc.set_precision("fp32")
+        torch.manual_seed(5)
+        _, m_fp32, _ = enc(x.to(cuda))
         enc.set_precision(enc_prec)
         m_or = torch.from_numpy(fx["c2_means"])
         q16, i16 = ic2.quantize_uniform(m16, 8, return_indices=True)
@@ -96,7 +101,7 @@ def c2(cuda):
         G.set_precision("fp32")
     return dict(enc=enc, G=G, x=x, m16=m16.cpu(), m_or=m_or, i16=i16.cpu().long(), q_or=q_or, ref=ref,
                 img_e2e=img_e2e, img_syn=img_syn, m_allbf16=m_allbf16.cpu(), img_e2e_f16=img_e2e_f16,
-                img_syn_f16=img_syn_f16)
+                img_syn_f16=img_syn_f16, m_fp32=m_fp32.cpu())
 
 
 def test_c2_reference_reconstruction_is_the_oracle(c2):
@@ -133,6 +138,20 @@ def test_c2_bench_indices_vs_oracle(c2):
     assert err.max().item() < ENC_TOL
     assert d.abs().max().item() <= 1
     assert frac <= IDX_FRAC
+    assert int(mism.sum()) <= IDX_COUNT_BENCH
+    assert (dist <= HALF_STEP).all()
+
+
+def test_c2_fp32_mode_indices_vs_oracle(c2):
+    """The fp32 parity mode (exact-f32 MFMA encoder) on the C2 batch: a count bar of its own, tighter than the benched
+    mode's, every flip by one and at a half-step."""
+    err, d, mism, dist = _index_stats(c2["m_fp32"], c2["m_or"])
+    print(f"[c2] encoder (fp32 mode) vs oracle: max|dm| = {err.max().item():.3e}, index mismatches "
+          f"{int(mism.sum())}/{mism.numel()}, max half-step distance of a mismatch = "
+          f"{dist.max().item() if dist.numel() else 0.0:.3e}")
+    assert err.max().item() < ENC_TOL
+    assert d.abs().max().item() <= 1
+    assert int(mism.sum()) <= IDX_COUNT_FP32
     assert (dist <= HALF_STEP).all()
 
 

@@ -182,6 +182,9 @@ def test_encoder_small_matches_reference(cuda, golden_dir):
     assert enc.fine_projector.fc1.weight.shape == (256, 16)
 
 
+FULL_CONFIG_INDEX_BAR = {"fp32": 4, "bf16x3": 8}
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 def test_encoder_full_config_matches_reference(cuda, golden_dir, precision):
     """HVAE_VGG_Encoder(img_resolution=1024) at seed 0 on 256^2 input (seed 1): reference latents, in the fp32
@@ -206,9 +209,10 @@ def test_encoder_full_config_matches_reference(cuda, golden_dir, precision):
     if mism.any():
         frac = ((om_[mism] + 1) * 0.5 * 255) % 1.0
         assert ((frac - 0.5).abs() < 1e-3).all()
-    # the tiered index bar of SURVEY.md 7 / test_gpu_c2_parity.IDX_FRAC (split mode measured: 6 of 16384 here)
+    # a count bar per precision: the fp32 parity mode keeps its round-4 bar; the benched
+    # split-bf16 mode measured 6 of 16384 here in round 5, plus a margin of 2
     print(f"[encoder full config, {precision}] index mismatches {mism.sum().item()} / {mism.numel()}")
-    assert mism.float().mean().item() <= 1e-3
+    assert mism.sum().item() <= FULL_CONFIG_INDEX_BAR[precision]
 
 
 def test_encoder_bf16_close_to_fp32(cuda):

@@ -87,13 +87,43 @@ def test_conv_wino_matches_fp64(cuda, case, layout, out_dt, act):
     assert torch.isfinite(yw).all()
 
 
-def test_conv_wino_leaves_padding_channels_and_bounds(cuda):
-    """Stores stay inside the tensor: the NHWC16 output's padded channel block and nothing past the end is written
-    (the output buffer is pre-filled with 7; padded output channels carry bias 0 * acc = the bias of a zero row)."""
+@pytest.mark.parametrize("layout", [nv.NHWC16, nv.NHWC], ids=["nhwc16", "nhwc"])
+def test_conv_wino_leaves_padding_channels_and_bounds(cuda, layout):
+    """Stores stay inside the tensor: the output is a view into a buffer with sentinel guard bands
+    of GUARD elements before and after it; the kernel's input reads deliberately run past the halo lines
+    (csrc/wino.hip:41,146), so its stores are checked here.  After the launch both guards are bit-unchanged, every
+    valid channel was written (no 7.0 sentinel left), and the padded output channels 40..63 (zero U rows) hold
+    0 * acc * oscale + bias = the f16-rounded bias."""
+    n, ci, co, cop, s, pad = 2, 64, 40, 64, 17, 2
+    ho = s + 2 * pad - 2
+    GUARD = 8192
+    g = torch.Generator(device=cuda).manual_seed(11)
+    cip = nv.pad32(ci)
+    x = torch.zeros(n, s, s, cip, device=cuda, dtype=torch.float16)
+    x[..., :ci] = torch.randn(n, s, s, ci, device=cuda, generator=g).to(torch.float16)
+    w = torch.randn(co, ci, 3, 3, device=cuda, generator=g)
+    st = nv.stream_of(x)
+    u = torch.empty(cop, 3, 4, cip, device=cuda, dtype=torch.float16)
+    nv.call("ic2_pack_weight_wino", nv.ptr(w), co, ci, cop, cip, 1, 1.0, nv.ptr(u), nv.F16, st)
+    osc = (torch.rand(n, cop, device=cuda, generator=g) + 0.5) / (9 * ci) ** 0.5
+    bias = torch.randn(cop, device=cuda, generator=g) * 0.1
+    shape = [n, cop // 16, ho, ho, 16] if layout == nv.NHWC16 else [n, ho, ho, cop]
+    numel = n * ho * ho * cop
+    base = torch.full([GUARD + numel + GUARD], -1234.5, device=cuda, dtype=torch.float16)
+    base[GUARD:GUARD + numel] = 7.0
+    y = base[GUARD:GUARD + numel].view(shape)
+    assert y.data_ptr() % 16 == 0
     with torch.no_grad():
-        _, _, _, yw = _run(cuda, 2, 64, 40, 17, 2, nv.NHWC16, torch.float16, False, cout_p=64)
-    # cout 40 -> padded channels 40..63 hold acc 0 * oscale + bias (the kernel writes every channel < cout_p)
-    assert torch.isfinite(yw).all()
+        nv.conv_wino(nv.ptr(x), nv.ptr(u), nv.ptr(y), nv.F16, nv.F16, n, s, s, cip, cop, co, pad, ho, ho, nv.ptr(osc),
+                     nv.ptr(bias), 0, 0.0, 1.0, -1.0, 1.0, layout, st)
+    torch.cuda.synchronize()
+    b = base.cpu()
+    assert (b[:GUARD] == -1234.5).all() and (b[GUARD + numel:] == -1234.5).all(), "store outside the output tensor"
+    yc = y.cpu().float()
+    yc = yc.permute(0, 1, 4, 2, 3).reshape(n, cop, ho, ho) if layout == nv.NHWC16 else yc.permute(0, 3, 1, 2)
+    assert not (yc[:, :co] == 7.0).any(), "a valid output was not written"
+    pad_ref = bias[co:].to(torch.float16).float().cpu()[None, :, None, None].expand(n, cop - co, ho, ho)
+    assert torch.equal(yc[:, co:], pad_ref)
 
 
 def test_conv_wino_plan_names_a_tile(cuda):

@@ -260,6 +260,82 @@ def test_grad_reducer_overlapped_matches_post_backward_allreduce(tmp_path):
             assert d["unused"]
 
 
+class _C5Encoder(torch.nn.Module):
+    """BASELINE C5's encoder (HVAE_VGG_Encoder(img_resolution=1024), ref stylegan3_hvae_full.py:34-103) with the
+    oracle's torch restatement of its forward (ref :105-167) over the live parameters, so it runs on the CPU: on a 256^2
+    input the 1x1 break (ref :129-131) stops before blocks 8-9, which get no gradient.  The fine projector's fc1 is
+    re-created per call as the reference does (:225-230), seeded the same on every rank (broadcast in the product)."""
+
+    def __init__(self):
+        super().__init__()
+        import image_compression_2_amd as ic2
+        self.enc = ic2.HVAE_VGG_Encoder(img_resolution=1024)
+
+    def forward(self, x):
+        from oracle import encoder as oe
+        sd = dict(self.enc.named_parameters())
+        g = torch.Generator().manual_seed(7)
+        fc1 = torch.nn.Linear(128, 256)
+        with torch.no_grad():
+            fc1.weight.copy_(torch.randn(256, 128, generator=g) * 0.05)
+            fc1.bias.zero_()
+        self.enc.fine_projector.fc1 = fc1
+        return oe.encoder_forward(sd, x, fine_fc1=(fc1.weight, fc1.bias))
+
+
+def _c5_reducer_worker(out_path):
+    import torch.distributed as dist
+    rank, world, _ = icd.init("gloo")
+    torch.manual_seed(0)   # same weights on every rank
+    m = _C5Encoder()
+    r = icd.GradReducer(m, world)   # the training step's 25 MiB buckets
+    res = {}
+    for step in range(3):
+        x = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(10 * step + rank)) * 2 - 1
+        m.zero_grad(set_to_none=True)
+        w, mean, lv = m(x)
+        loss = w.square().mean() + 0.01 * (mean.square() + lv.exp() - lv).mean()
+        r.start()
+        loss.backward()
+        launched, nb = r.next_launch, len(r.buckets)
+        r.finish()
+        got = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        m.zero_grad(set_to_none=True)
+        w, mean, lv = m(x)
+        (w.square().mean() + 0.01 * (mean.square() + lv.exp() - lv).mean()).backward()
+        icd.allreduce_gradients(list(m.parameters()), world)
+        ref = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        res[step] = {"got": got, "ref": ref, "launched": launched, "nb": nb}
+    unused = [k for k, p in m.named_parameters() if p.grad is None]
+    torch.save({"steps": res, "unused": unused, "n_buckets": len(r.buckets)}, f"{out_path}.{rank}")
+    r.remove()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_overlaps_at_c5_config(tmp_path):
+    """at C5's own encoder config (1024 encoder on 256^2, blocks 8-9 unused) the first step's
+    registration-order buckets cannot launch during backward (bucket 0 waits for blocks 8-9); after the rebuild from
+    the hook order every bucket launches inside backward, and the gradients equal allreduce_gradients' on both ranks."""
+    out = str(tmp_path / "c5")
+    icd.launch(2, _c5_reducer_worker, out)
+    res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    assert any(k.startswith("enc.blocks.8.") for k in res[0]["unused"])
+    assert any(k.startswith("enc.blocks.9.") for k in res[0]["unused"])
+    assert res[0]["n_buckets"] >= 5   # ~120 MB of used f32 gradients in 25 MiB buckets
+    for rk in range(2):
+        steps = res[rk]["steps"]
+        for step in range(3):
+            d = steps[step]
+            assert set(d["got"]) == set(d["ref"])
+            for k in d["ref"]:
+                assert torch.allclose(d["got"][k], d["ref"][k], rtol=1e-5, atol=1e-8), (step, k)
+                assert torch.equal(d["got"][k], res[0]["steps"][step]["got"][k]), ("ranks disagree", step, k)
+        assert steps[0]["launched"] == 0   # registration order: bucket 0 holds blocks 8-9
+        for step in (1, 2):
+            assert steps[step]["launched"] == steps[step]["nb"] == res[0]["n_buckets"], steps[step]["launched"]
+
+
 def test_grad_reducer_single_process_is_inert():
     m = _ToyEncoder()
     r = icd.GradReducer(m, world=1)

@@ -2,7 +2,9 @@
 # Bench evidence for a round: C2 (default precision) and C4/C5 bench lines, rocprofv3 kernel traces (+ --stats) of C2
 # and C4 split into timed steps by tools/trace_steps.py, and the PMC HBM traffic of the C2 conv family
 # (tools/pmc_traffic.sh).  Each GPU step has its own time limit; the script stops at the first failure.
-#   bash tools/gpu_evidence.sh <tag> [c2 c4 c5 trace trace5 pmc]     (default: c2 c4 c5 trace pmc)
+#   bash tools/gpu_evidence.sh <tag> [tests [K] smoke c2 c4 c5 trace trace5 pmc pmc4]   (default: c2 c4 c5 trace pmc)
+# tests: the GPU pytest suite (optionally only `-k K`), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic.
+# (Replaces the round-5 one-shot gpu_*.sh scripts.)
 set -o pipefail
 cd $GRAFT_REPO_ROOT || exit 1
 tag=${1:-r4}; shift
@@ -15,8 +17,20 @@ run() {  # name, args...
   timeout -k 10 300 python bench.py "$@" --out $o/${tag}_$n.json > $o/${tag}_$n.log 2>&1 || { tail -20 $o/${tag}_$n.log; exit 1; }
   python3 -c "import json; d=json.load(open('$o/${tag}_$n.json')); r=d.get('roofline',{}); print('$n', d['value'], d['ms_per_step'], r.get('frac'), r.get('path_frac'), r.get('flr',{}).get('ms_per_step'), d.get('cpu_baseline',{}).get('value'))"
 }
-for p in $parts; do
+set -- $parts
+while [ $# -gt 0 ]; do
+  p=$1; shift
   case $p in
+    tests)
+      k=""
+      if [ $# -gt 0 ] && ! [[ " smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=$1; shift; fi
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${k:+-k "$k"} \
+        > $o/${tag}_pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $o/${tag}_pytest.log | tail -30; tail -30 $o/${tag}_pytest.log; exit 1; }
+      tail -2 $o/${tag}_pytest.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $o/${tag}_smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -20 $o/${tag}_smoke.log; exit 1; }
+      tail -1 $o/${tag}_smoke.log ;;
     c2) run c2 --steps 50 --warmup 10 ;;
     c4) run c4 --config c4 --steps 20 --warmup 5 ;;
     c5) run c5 --config c5 --steps 20 --warmup 5 --cpu-baseline-images 0 ;;
@@ -37,7 +51,8 @@ for p in $parts; do
         || { tail -20 $o/${tag}_prof_c5.log; exit 1; }
       find $o/prof_c5 -name "*kernel_stats.csv" -exec cp {} $o/${tag}_c5_kernel_stats.csv \;
       head -25 $o/${tag}_c5_kernel_stats.csv | cut -c1-160 ;;
-    pmc) bash tools/pmc_traffic.sh ${tag}_pmc_traffic_c2_f16_b32 || exit 1 ;;
+    pmc) bash tools/pmc_traffic.sh ${tag}_pmc_traffic_c2_f16_b32 --no-secondary || exit 1 ;;
+    pmc4) bash tools/pmc_traffic.sh ${tag}_pmc_traffic_c4_f16_b8 --config c4 || exit 1 ;;
   esac
 done
 echo "[evidence] done"

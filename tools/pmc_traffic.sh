@@ -5,7 +5,7 @@
 # usage: bash tools/pmc_traffic.sh <out-json-name> [bench args...]
 set -o pipefail
 name=${1:-pmc_traffic}; shift
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/pmc_traffic
+cd $GRAFT_REPO_ROOT && rm -rf gpurun_out/pmc_traffic/p1 gpurun_out/pmc_traffic/p2 && mkdir -p gpurun_out/pmc_traffic
 export TMPDIR=/tmp
 i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
