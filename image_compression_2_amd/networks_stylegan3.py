@@ -479,11 +479,12 @@ class SynthesisLayer(torch.nn.Module):
         self._cache[("adj", dt)] = (key, wt)
         return wt
 
-    def packed_adjoint_wino(self):
+    def packed_adjoint_wino(self, scale=1.0):
         """packed_adjoint for the Winograd kernel: U [cin_p][3][4][cout_p] f16 of the normalised W flipped in space
-        and transposed in channels (ic2_pack_weight_wino on the f32 adjoint, no further normalisation)."""
-        key = _version_key(self.weight)
-        hit = self._cache.get("adj_wino")
+        and transposed in channels (ic2_pack_weight_wino on the f32 adjoint, no further normalisation), times `scale`
+        (a power of two: the training dgrad packs 2 U against a halved dc, autograd_ops._synth_layer_grads)."""
+        key = (_version_key(self.weight), scale)
+        hit = self._cache.get(("adj_wino", scale))
         if hit is not None and hit[0] == key:
             return hit[1]
         w = self.weight.detach().to(torch.float32)
@@ -492,8 +493,8 @@ class SynthesisLayer(torch.nn.Module):
         wa = w.transpose(0, 1).flip(2, 3).contiguous()
         u = torch.empty([self.cin_p, 3, 4, self.cout_p], dtype=torch.float16, device=w.device)
         nv.call("ic2_pack_weight_wino", nv.ptr(wa), self.in_channels, self.out_channels, self.cin_p, self.cout_p, 0,
-                1.0, nv.ptr(u), nv.F16, nv.stream_of(wa))
-        self._cache["adj_wino"] = (key, u)
+                float(scale), nv.ptr(u), nv.F16, nv.stream_of(wa))
+        self._cache[("adj_wino", scale)] = (key, u)
         return u
 
     def modulation_train(self, w):

@@ -1,6 +1,7 @@
 """ic2_conv_wino (fused Winograd F(2,3) along x, f16 MFMA) against an fp64 conv of the same operands, next to the
 direct f16 implicit GEMM on the same inputs.  Reference: the grouped conv2d of modulated_conv2d [SG3-public] in
 its activation-scaling form (stylegan3_hvae_full.py:274,329), i.e. ic2_conv_igemm's contract for 3x3."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -164,3 +165,68 @@ def test_wino_adjoint_dgrad_matches_fp64(cuda):
     assert e_w < 4e-3 and e_w <= 4 * e_d + 1e-4, (e_w, e_d)
     if L.cin_p > L.in_channels:  # padded input channels: zero adjoint rows
         assert da_w[..., L.in_channels:].abs().max().item() == 0.0
+
+
+def _adjoint_layer(cuda):
+    from image_compression_2_amd.networks_stylegan3 import SynthesisLayer
+    torch.manual_seed(0)
+    return SynthesisLayer(w_dim=512, is_torgb=False, is_critically_sampled=False, use_fp16=False, in_channels=250,
+                          out_channels=320, in_size=50, out_size=50, in_sampling_rate=16, out_sampling_rate=16,
+                          in_cutoff=8, out_cutoff=8, in_half_width=4, out_half_width=4).to(cuda)
+
+
+def test_wino_dgrad_halved_operand_keeps_f16_headroom(cuda):
+    """V = B^T dc is formed with f16 adds, so dc values of opposite sign near the f16 limit overflow in V
+    where the direct implicit GEMM (f16 products, f32 sums) stays finite.  The training dgrad therefore runs the kernel
+    on dc / 2 against U packed times 2 (autograd_ops._synth_layer_grads).  Here dc alternates +-60000 along x: on the
+    raw operand the Winograd result overflows; on the halved one it is finite and matches the direct GEMM on dc."""
+    from image_compression_2_amd import autograd_ops as ao
+    L = _adjoint_layer(cuda)
+    n, conv = 2, 52
+    g = torch.Generator(device=cuda).manual_seed(5)
+    mag = 40000 + 20000 * torch.rand(n, conv, conv, L.out_channels, device=cuda, generator=g)
+    sign = torch.ones(conv, device=cuda)
+    sign[1::2] = -1
+    dc = torch.zeros(n, conv, conv, L.cout_p, device=cuda, dtype=torch.float16)
+    dc[..., :L.out_channels] = (mag * sign[None, None, :, None]).to(torch.float16)
+    with torch.no_grad():
+        d_direct = ao.conv_nhwc(dc, L.packed_adjoint(torch.float16), None, L.in_channels, 3, 0, dt_out=torch.float32)
+        d_raw = ao.conv_nhwc(dc, L.packed_adjoint(torch.float16), None, L.in_channels, 3, 0, dt_out=torch.float32,
+                             wino=L.packed_adjoint_wino)
+        d_half = ao.conv_nhwc(dc * 0.5, L.packed_adjoint(torch.float16), None, L.in_channels, 3, 0,
+                              dt_out=torch.float32, wino=lambda: L.packed_adjoint_wino(2.0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(d_direct).all()
+    assert not torch.isfinite(d_raw).all()          # the hazard the halving removes
+    assert torch.isfinite(d_half).all()
+    ref = d_direct[..., :L.in_channels].double()
+    err = (d_half[..., :L.in_channels].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 4e-3, err
+
+
+def test_synth_layer_dgrad_scales_exactly_to_the_f16_limit(cuda):
+    """The training path's layer backward (_synth_layer_grads, Winograd dgrad on the halved dc) is linear in the upstream
+    gradient up to the f16 limit of dc: scaling it by 2^k so that max|dc| lies in [2^15, 2^16) gives a finite dL/da
+    equal to 2^k times the unscaled one (power-of-two scaling is exact away from f16 subnormals: rtol 1e-3)."""
+    from image_compression_2_amd import autograd_ops as ao
+    L = _adjoint_layer(cuda)
+    n, conv, s_out = 2, 52, 50
+    assert nv.wino_preferred(nv.F16, n, conv, conv, L.cout_p, L.cin_p, 3, 3, 0)
+    g = torch.Generator(device=cuda).manual_seed(6)
+    y = torch.zeros(n, conv, conv, L.cout_p, device=cuda, dtype=torch.float16)
+    y[..., :L.out_channels] = (torch.randn(n, conv, conv, L.out_channels, device=cuda, generator=g) * 2).to(torch.float16)
+    dout = torch.zeros(n, s_out, s_out, L.cout_p, device=cuda, dtype=torch.float16)
+    dout[..., :L.out_channels] = torch.randn(n, s_out, s_out, L.out_channels, device=cuda, generator=g).to(torch.float16)
+    os_ = (torch.rand(n, L.cout_p, device=cuda, generator=g) + 0.5).contiguous()
+    with torch.no_grad():
+        gy = ao._flrelu_backward_composed(y, dout, L)
+        dcmax = (gy * os_[:, None, None, :]).abs().max().item()
+        k = int(np.floor(np.log2(65000 / dcmax)))
+        assert 2 ** 15 <= dcmax * 2 ** k < 2 ** 16
+        da1, dos1 = ao._synth_layer_grads(L, torch.float16, os_, y, dout)
+        dak, dosk = ao._synth_layer_grads(L, torch.float16, os_, y, (dout.float() * 2 ** k).to(torch.float16))
+    torch.cuda.synchronize()
+    assert torch.isfinite(dak).all() and torch.isfinite(dosk).all()
+    a1, ak = da1[..., :L.in_channels].float() * 2 ** k, dak[..., :L.in_channels].float()
+    assert torch.allclose(ak, a1, rtol=1e-3, atol=1e-3 * a1.abs().max().item()), (ak - a1).abs().max().item()
+    assert torch.allclose(dosk, dos1 * 2 ** k, rtol=1e-3, atol=1e-3 * (dos1 * 2 ** k).abs().max().item())

@@ -3,7 +3,9 @@
 # and C4 split into timed steps by tools/trace_steps.py, and the PMC HBM traffic of the C2 conv family
 # (tools/pmc_traffic.sh).  Each GPU step has its own time limit; the script stops at the first failure.
 #   bash tools/gpu_evidence.sh <tag> [tests [K] smoke c2 c4 c5 trace trace5 pmc pmc4]   (default: c2 c4 c5 trace pmc)
-# tests: the GPU pytest suite (optionally only `-k K`), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic.
+# tests: the GPU pytest suite (optionally only `-k K`), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic,
+# abwino <tag>: the Winograd conv of image_compression_2_amd/libic2ops_<tag>.so (tools/build_abl.sh) against the default
+# library -- tests/test_gpu_wino.py on the variant, then tools/bench_wino.py on both, alternating, two rounds.
 # (Replaces the round-5 one-shot gpu_*.sh scripts.)
 set -o pipefail
 cd $GRAFT_REPO_ROOT || exit 1
@@ -23,10 +25,22 @@ while [ $# -gt 0 ]; do
   case $p in
     tests)
       k=""
-      if [ $# -gt 0 ] && ! [[ " smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=$1; shift; fi
+      if [ $# -gt 0 ] && ! [[ " abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=$1; shift; fi
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${k:+-k "$k"} \
         > $o/${tag}_pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $o/${tag}_pytest.log | tail -30; tail -30 $o/${tag}_pytest.log; exit 1; }
       tail -2 $o/${tag}_pytest.log ;;
+    abwino)
+      v=$1; shift
+      IC2_DEV=1 IC2_DEV_LIB=image_compression_2_amd/libic2ops_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_wino.py \
+        -x -q --timeout 120 --timeout-method thread > $o/${tag}_ab_$v.log 2>&1 || { echo "variant tests failed"; tail -30 $o/${tag}_ab_$v.log; exit 1; }
+      tail -1 $o/${tag}_ab_$v.log
+      for rnd in 1 2; do
+        for lib in libic2ops libic2ops_$v; do
+          IC2_DEV=1 IC2_DEV_LIB=image_compression_2_amd/$lib.so timeout -k 10 300 python -u tools/bench_wino.py s52 s84 s148 s148b s148c \
+            > $o/${tag}_ab_${lib}_$rnd.log 2>&1 || { echo "bench_wino failed ($lib)"; tail -20 $o/${tag}_ab_${lib}_$rnd.log; exit 1; }
+          echo "== $lib round $rnd"; grep -E "wino" $o/${tag}_ab_${lib}_$rnd.log | tail -6
+        done
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $o/${tag}_smoke.log 2>&1 \
         || { echo "smoke failed"; tail -20 $o/${tag}_smoke.log; exit 1; }
