@@ -19,6 +19,7 @@ if os.environ.get("IC2_DEV") == "1" and os.environ.get("IC2_DEV_LIB"):
     LIB_PATH = os.environ["IC2_DEV_LIB"]
 
 F32, BF16, F16, BF16X3, F16X2 = 0, 1, 2, 3, 4
+F16_IEEE = 5   # out_dtype only: f16 output converted IEEE (overflow -> inf), the training path's gradient convs
 ACT_LINEAR, ACT_LRELU = 0, 1
 NHWC, NCHW, NHWC16 = 0, 1, 2
 

@@ -96,20 +96,23 @@ class SplitRows(torch.autograd.Function):
         return g, None
 
 
-def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None, wino=None):
+def conv_nhwc(x, wp, bias_p, cout_valid, kh, pad, dt_out=None, wino=None, grad=False):
     """Conv on NHWC x with packed weights wp [cout_p][kh][kh][cin_p].  wino: a callable returning the same weights
-    packed for the Winograd kernel (U [cout_p][3][4][cin_p] f16), used where ic2_conv_wino_preferred picks it."""
+    packed for the Winograd kernel (U [cout_p][3][4][cin_p] f16), used where ic2_conv_wino_preferred picks it.
+    grad: the output is a gradient -- an f16 output is converted IEEE (overflow -> inf, which the loss scaler must
+    see) instead of saturated at +-65504 like an activation."""
     n, h, w, cin_p = x.shape
     cout_p = wp.shape[0]
     ho, wo = h + 2 * pad - kh + 1, w + 2 * pad - kh + 1
     dt_out = x.dtype if dt_out is None else dt_out
     y = torch.empty([n, ho, wo, cout_p], dtype=dt_out, device=x.device)
+    odt = nv.F16_IEEE if grad and dt_out == torch.float16 else nv.dtype_code(dt_out)
     if wino is not None and nv.wino_preferred(nv.dtype_code(x.dtype), n, h, w, cin_p, cout_p, kh, kh, pad):
-        nv.conv_wino(nv.ptr(x), nv.ptr(wino()), nv.ptr(y), nv.dtype_code(x.dtype), nv.dtype_code(dt_out), n, h, w,
+        nv.conv_wino(nv.ptr(x), nv.ptr(wino()), nv.ptr(y), nv.dtype_code(x.dtype), odt, n, h, w,
                      cin_p, cout_p, cout_valid, pad, ho, wo, None, nv.ptr(bias_p), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
                      nv.stream_of(x))
         return y
-    nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.dtype), nv.dtype_code(dt_out), n, h, w, cin_p,
+    nv.conv_igemm(nv.ptr(x), nv.ptr(wp), nv.ptr(y), nv.dtype_code(x.dtype), odt, n, h, w, cin_p,
                   cout_p, cout_valid, kh, kh, pad, ho, wo, None, nv.ptr(bias_p), 0, 0.0, 1.0, -1.0, 1.0, nv.NHWC,
                   nv.stream_of(x), x.device)
     return y
@@ -151,7 +154,7 @@ class Conv2dNHWC(torch.autograd.Function):
             # dx = conv(dy, W flipped in space, transposed in channels), padding k - 1 - pad
             wtp = _derived(ctx.weight, ("adj", cin_p, cout_p, x.dtype),
                            lambda: pack_conv_weight(weight.detach().transpose(0, 1).flip(2, 3), cout_p, cin_p, x.dtype))
-            dx = conv_nhwc(dy, wtp, None, cin_p, kh, kh - 1 - ctx.pad)
+            dx = conv_nhwc(dy, wtp, None, cin_p, kh, kh - 1 - ctx.pad, grad=True)
         if ctx.needs_input_grad[1]:
             nfl = int(nv.query("ic2_conv_wgrad_ws_floats", n, h, w, cin_p, cout_p, kh, kw, ctx.pad))
             ws = torch.empty([max(nfl, 4)], dtype=torch.float32, device=x.device)
@@ -303,7 +306,7 @@ def _synth_layer_grads(L, dt, os_, y, dout, post=None):
     # dL/da: the implicit GEMM on the adjoint weights (valid conv: the forward padded by k - 1); the Winograd kernel
     # (where ic2_conv_wino_preferred picks it, the condition of `halve`) on 2 U against dc / 2
     da = conv_nhwc(dc, L.packed_adjoint(dt), None, L.in_channels, L.conv_kernel, 0,
-                   wino=(lambda: L.packed_adjoint_wino(2.0)) if halve else None)
+                   wino=(lambda: L.packed_adjoint_wino(2.0)) if halve else None, grad=True)
     return da, d_os
 
 
@@ -410,7 +413,7 @@ class FrozenConvNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         k, pad, cin, dt = ctx.meta
-        dx = conv_nhwc(dy.to(dt).contiguous(), ctx.wt, None, cin, k, k - 1 - pad)
+        dx = conv_nhwc(dy.to(dt).contiguous(), ctx.wt, None, cin, k, k - 1 - pad, grad=True)
         return dx, None, None, None, None, None, None
 
 

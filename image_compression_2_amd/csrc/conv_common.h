@@ -56,6 +56,9 @@ struct IgemmArgs {
   // served by wx_ns 16-lane pair blocks; halo line pitch wx_hp (64-B LDS rows per (halo row, column parity) line),
   // wx_nh halo rows used, wx_tx x wx_ty tiles per image
   int wx_twp, wx_th, wx_ns, wx_hp, wx_nh, wx_tx, wx_ty;
+  // f16 output converted IEEE (out_dtype IC2_F16_IEEE at the entry point: the training path's gradient convs) instead
+  // of saturated to the f16 range (activations)
+  int out_ieee;
 };
 __device__ __forceinline__ int ig_xb32(const IgemmArgs& a, int b) { return b >= a.x_hb32 ? b - a.x_hb32 : b; }
 
@@ -106,7 +109,7 @@ __device__ __forceinline__ void ig_store4v(const IgemmArgs& a, int p, int nn, in
       typedef _Float16 h2 __attribute__((ext_vector_type(2)));
       float s_[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s_[r] = __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
+      for (int r = 0; r < 4; ++r) s_[r] = a.out_ieee ? v[r] : __builtin_amdgcn_fmed3f(v[r], -65504.f, 65504.f);
       const h2 q0 = h2{(_Float16)s_[0], (_Float16)s_[1]}, q1 = h2{(_Float16)s_[2], (_Float16)s_[3]};
       if (vout != nullptr) {  // the statistics of what is stored (the f16 values), as the separate pass sees them
         (*vout)[0] = (float)q0.x; (*vout)[1] = (float)q0.y; (*vout)[2] = (float)q1.x; (*vout)[3] = (float)q1.y;

@@ -1667,7 +1667,8 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
                 "conv_igemm: split-bf16 input needs cin_p = 3 x a multiple of 32 and NHWC output (cin_p=%d)", cin_p);
   IC2_CHECK_ARG(dtype != IC2_F16X2 || (cin_p % 64 == 0 && out_layout == IC2_LAYOUT_NHWC),
                 "conv_igemm: split-weight f16 input needs cin_p = 2 x a multiple of 32 and NHWC output (cin_p=%d)", cin_p);
-  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
+  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 ||
+                    ((out_dtype == IC2_F16 || out_dtype == IC2_F16_IEEE) && out_layout != IC2_LAYOUT_NCHW),
                 "conv_igemm: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
                 "conv_igemm: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
@@ -1697,13 +1698,15 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   }
   const int64_t M = (int64_t)n * ho * wo;
   IC2_CHECK_ARG(M < (1LL << 30), "conv_igemm: too many output pixels");
+  const int out_ieee = out_dtype == IC2_F16_IEEE;
+  if (out_ieee) out_dtype = IC2_F16;
   IgemmArgs a;
   a.x = x; a.w = w; a.y = y; a.oscale = oscale; a.bias = bias; a.ws = reinterpret_cast<float*>(workspace);
   a.n = n; a.h = h; a.w_ = w_; a.cin_p = cin_p; a.cout_p = cout_p; a.cout_valid = cout_valid;
   a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
-  a.out_layout = out_layout; a.out_dtype = out_dtype;
+  a.out_layout = out_layout; a.out_dtype = out_dtype; a.out_ieee = out_ieee;
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0;
   a.in_gn = nullptr; a.in_slope = 0.f;
   a.x_pix = x_pix_of(dtype, cin_p);
@@ -1835,7 +1838,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
     a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
     a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
     a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = out_mul;
-    a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = ydt;
+    a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = ydt; a.out_ieee = 0;
     a.gn_part = part; a.gn_groups = groups; a.gn_c = cout_valid;
     a.group = 1; a.korder = 0; a.o_base = 0;
     a.in_gn = nullptr; a.in_slope = 0.f;
@@ -1884,7 +1887,7 @@ int conv_gn_fused(const void* x, const void* w, void* y, int dtype, int n, int h
   a.kh = kh; a.kw = kw; a.pad = pad; a.ho = ho; a.wo = wo;
   a.M = (int)M; a.K = kh * kw * cin_p; a.nq = a.K / 32;
   a.act = 0; a.slope = 0.f; a.act_gain = 1.f; a.clamp = -1.f; a.out_mul = 1.f;
-  a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = dtype;
+  a.out_layout = IC2_LAYOUT_NHWC; a.out_dtype = dtype; a.out_ieee = 0;
   a.gn_part = fuse ? part : nullptr; a.gn_groups = groups; a.gn_c = cout_valid;
   a.group = 1;
   a.korder = 0;

@@ -578,7 +578,8 @@ extern "C" int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, i
                              int out_layout, void* stream) {
   IC2_CHECK_ARG(x && u && y, "conv_wino: null pointer");
   IC2_CHECK_ARG(dtype == IC2_F16, "conv_wino: f16 operands only (dtype %d)", dtype);
-  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 || (out_dtype == IC2_F16 && out_layout != IC2_LAYOUT_NCHW),
+  IC2_CHECK_ARG(out_dtype == IC2_F32 || out_dtype == IC2_BF16 ||
+                    ((out_dtype == IC2_F16 || out_dtype == IC2_F16_IEEE) && out_layout != IC2_LAYOUT_NCHW),
                 "conv_wino: bad out dtype %d", out_dtype);
   IC2_CHECK_ARG(cin_p > 0 && cin_p % 32 == 0 && cout_p > 0 && cout_p % 32 == 0,
                 "conv_wino: channel strides must be positive multiples of 32 (cin_p=%d cout_p=%d)", cin_p, cout_p);
@@ -607,6 +608,8 @@ extern "C" int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, i
   }
   const WxTile t = wx_tile(n, ho, wo, cout_p);
   IC2_CHECK_ARG(t.blocks > 0 && t.blocks < (1LL << 31), "conv_wino: bad tile plan");
+  const int out_ieee = out_dtype == IC2_F16_IEEE;
+  if (out_ieee) out_dtype = IC2_F16;
   IgemmArgs a{};
   a.x = x; a.w = u; a.y = y; a.oscale = oscale; a.bias = bias;
   a.ws = IC2_WX_STAMP && (int64_t)t.blocks * 8 * 8 * 8 <= g_wx_stamp_bytes ? reinterpret_cast<float*>(g_wx_stamp)
@@ -622,7 +625,7 @@ extern "C" int ic2_conv_wino(const void* x, const void* u, void* y, int dtype, i
   while (t.to % og) --og;
   a.tiles_o = t.to; a.nblocks = (int)t.blocks; a.group = og; a.korder = 1; a.o_base = 0;
   a.act = act; a.slope = slope; a.act_gain = act_gain; a.clamp = clamp; a.out_mul = out_mul;
-  a.out_layout = out_layout; a.out_dtype = out_dtype;
+  a.out_layout = out_layout; a.out_dtype = out_dtype; a.out_ieee = out_ieee;
   a.gn_part = nullptr; a.gn_groups = 0; a.gn_c = 0; a.in_gn = nullptr; a.in_slope = 0.f;
   a.x_pix = cin_p; a.x_hb32 = 0;
   a.wx_twp = t.twp; a.wx_th = t.th; a.wx_ns = t.ns; a.wx_hp = t.hp; a.wx_nh = t.nh; a.wx_tx = t.tx; a.wx_ty = t.ty;

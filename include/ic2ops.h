@@ -35,7 +35,12 @@ extern "C" {
 #endif
 
 enum { IC2_OK = 0, IC2_E_INVALID = 1, IC2_E_UNSUPPORTED = 2, IC2_E_LAUNCH = 3 };
-enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2, IC2_BF16X3 = 3, IC2_F16X2 = 4 };
+enum { IC2_F32 = 0, IC2_BF16 = 1, IC2_F16 = 2, IC2_BF16X3 = 3, IC2_F16X2 = 4,
+       /* an out_dtype of ic2_conv_igemm / ic2_conv_igemm_ws / ic2_conv_wino only: f16 output converted IEEE (an
+        * overflow stores +-inf instead of saturating at +-65504) -- the gradient convs of the f16 training path, so a
+        * loss-scaled gradient that overflows reaches the GradScaler as inf (the reference's fp16 autocast behaviour,
+        * stylegan3_hvae_full.py:693-696) */
+       IC2_F16_IEEE = 5 };
 enum { IC2_ACT_LINEAR = 0, IC2_ACT_LRELU = 1 };
 /* NHWC16: channel-blocked NHWC, [n][c_p / 16][h][w][16] (the synthesis conv -> fused filtered lrelu hand-off) */
 enum { IC2_LAYOUT_NHWC = 0, IC2_LAYOUT_NCHW = 1, IC2_LAYOUT_NHWC16 = 2 };

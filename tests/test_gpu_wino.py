@@ -204,10 +204,12 @@ def test_wino_dgrad_halved_operand_keeps_f16_headroom(cuda):
     assert err < 4e-3, err
 
 
-def test_synth_layer_dgrad_scales_exactly_to_the_f16_limit(cuda):
-    """The training path's layer backward (_synth_layer_grads, Winograd dgrad on the halved dc) is linear in the upstream
-    gradient up to the f16 limit of dc: scaling it by 2^k so that max|dc| lies in [2^15, 2^16) gives a finite dL/da
-    equal to 2^k times the unscaled one (power-of-two scaling is exact away from f16 subnormals: rtol 1e-3)."""
+def test_synth_layer_dgrad_overflow_reaches_the_scaler_as_inf(cuda):
+    """The training path's layer backward (_synth_layer_grads: Winograd dgrad on the halved dc, f16 output converted
+    IEEE) is linear in the upstream gradient up to the f16 limit of dL/da: scaled by 2^k so that max|dL/da| lies in
+    [2^15, 2^16) it equals 2^k times the unscaled result (power-of-two scaling is exact away from f16 subnormals: rtol
+    1e-3), and scaled 4x further it overflows to inf -- not to a saturated +-65504, which a GradScaler would take for a
+    clean step (the gradient convs' IC2_F16_IEEE output; activations keep saturating)."""
     from image_compression_2_amd import autograd_ops as ao
     L = _adjoint_layer(cuda)
     n, conv, s_out = 2, 52, 50
@@ -216,17 +218,25 @@ def test_synth_layer_dgrad_scales_exactly_to_the_f16_limit(cuda):
     y = torch.zeros(n, conv, conv, L.cout_p, device=cuda, dtype=torch.float16)
     y[..., :L.out_channels] = (torch.randn(n, conv, conv, L.out_channels, device=cuda, generator=g) * 2).to(torch.float16)
     dout = torch.zeros(n, s_out, s_out, L.cout_p, device=cuda, dtype=torch.float16)
-    dout[..., :L.out_channels] = torch.randn(n, s_out, s_out, L.out_channels, device=cuda, generator=g).to(torch.float16)
+    dout[..., :L.out_channels] = (torch.randn(n, s_out, s_out, L.out_channels, device=cuda, generator=g) * 1e-3).to(
+        torch.float16)
     os_ = (torch.rand(n, L.cout_p, device=cuda, generator=g) + 0.5).contiguous()
-    with torch.no_grad():
-        gy = ao._flrelu_backward_composed(y, dout, L)
-        dcmax = (gy * os_[:, None, None, :]).abs().max().item()
-        k = int(np.floor(np.log2(65000 / dcmax)))
-        assert 2 ** 15 <= dcmax * 2 ** k < 2 ** 16
-        da1, dos1 = ao._synth_layer_grads(L, torch.float16, os_, y, dout)
-        dak, dosk = ao._synth_layer_grads(L, torch.float16, os_, y, (dout.float() * 2 ** k).to(torch.float16))
+
+    def grads(k):
+        with torch.no_grad():
+            return ao._synth_layer_grads(L, torch.float16, os_, y, (dout.float() * 2.0 ** k).to(torch.float16))
+    da1, dos1 = grads(0)
     torch.cuda.synchronize()
+    m1 = da1[..., :L.in_channels].float().abs().max().item()
+    assert torch.isfinite(da1).all() and 0 < m1 < 2 ** 14
+    k = int(np.floor(np.log2(65000 / m1)))
+    dak, dosk = grads(k)
+    dak2, _ = grads(k + 2)
+    torch.cuda.synchronize()
+    assert 2 ** 15 <= m1 * 2 ** k < 2 ** 16
     assert torch.isfinite(dak).all() and torch.isfinite(dosk).all()
     a1, ak = da1[..., :L.in_channels].float() * 2 ** k, dak[..., :L.in_channels].float()
     assert torch.allclose(ak, a1, rtol=1e-3, atol=1e-3 * a1.abs().max().item()), (ak - a1).abs().max().item()
     assert torch.allclose(dosk, dos1 * 2 ** k, rtol=1e-3, atol=1e-3 * (dos1 * 2 ** k).abs().max().item())
+    assert torch.isinf(dak2).any()
+    assert not (dak2.abs() == 65504).any()

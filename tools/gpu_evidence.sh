@@ -3,7 +3,7 @@
 # and C4 split into timed steps by tools/trace_steps.py, and the PMC HBM traffic of the C2 conv family
 # (tools/pmc_traffic.sh).  Each GPU step has its own time limit; the script stops at the first failure.
 #   bash tools/gpu_evidence.sh <tag> [tests [K] smoke c2 c4 c5 trace trace5 pmc pmc4]   (default: c2 c4 c5 trace pmc)
-# tests: the GPU pytest suite (optionally only `-k K`), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic,
+# tests: the GPU pytest suite (optionally only `-k K`, K = comma-separated alternatives), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic,
 # abwino <tag>: the Winograd conv of image_compression_2_amd/libic2ops_<tag>.so (tools/build_abl.sh) against the default
 # library -- tests/test_gpu_wino.py on the variant, then tools/bench_wino.py on both, alternating, two rounds.
 # (Replaces the round-5 one-shot gpu_*.sh scripts.)
@@ -25,7 +25,8 @@ while [ $# -gt 0 ]; do
   case $p in
     tests)
       k=""
-      if [ $# -gt 0 ] && ! [[ " abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=$1; shift; fi
+      # K: a pytest -k expression without spaces, alternatives separated by commas (ddp,wino -> "ddp or wino")
+      if [ $# -gt 0 ] && ! [[ " abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=${1//,/ or }; shift; fi
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${k:+-k "$k"} \
         > $o/${tag}_pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $o/${tag}_pytest.log | tail -30; tail -30 $o/${tag}_pytest.log; exit 1; }
       tail -2 $o/${tag}_pytest.log ;;
