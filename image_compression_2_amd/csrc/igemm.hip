@@ -323,6 +323,10 @@ __device__ __forceinline__ int g8_off(int row, int chunk) { return row * 128 + (
 __device__ __forceinline__ int g8_arow(int qm, int g, int l) { return (g >> 3) * 128 + qm * 64 + (g & 7) * 8 + l; }
 __device__ __forceinline__ int g8_brow(int qn, int g, int l) { return (g >> 2) * 64 + qn * 32 + (g & 3) * 8 + l; }
 
+// IC2_G8_PF=1 (A/B build): the prefetch schedule (below); 0: fragments read in the phase that uses them
+#ifndef IC2_G8_PF
+#define IC2_G8_PF 0
+#endif
 template <int OG, bool F16 = false>
 __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   using G = G8<OG>;
@@ -512,6 +516,92 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 
   const int niter = (t_end - t_begin + 1) >> 1;
   Cur cn = c1;  // tile 2i+1
+#if IC2_G8_PF
+  // Prefetch schedule (IC2_G8_PF=1): a phase's new operand is read inside the PREVIOUS phase's MFMA section, each
+  // 16-row fragment group right behind the MFMAs that consumed its registers (no extra registers), so a phase's R
+  // section holds only its DMA issue and waits.  Legal: every half is read >= 0 phases after the vmcnt + barrier
+  // that retires it (buf1 at phase 3, buf0 at phase 7) and >= 2 phases before it is restaged.
+#define IC2_G8_READ_AI(buf_, qm_, i_)                                                                         \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s) af[i_][s] =                                                  \
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + g8_off(grp * 128 + (qm_) * 64 + (i_) * 16 + fr, 4 * s + fh));
+#define IC2_G8_READ_BJ(buf_, qn_, j_)                                                                         \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s) bfr[j_][s] =                                                 \
+      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + G::BOFF + g8_off(wp_ * 64 + (qn_) * 32 + (j_) * 16 + fr, 4 * s + fh));
+#define IC2_G8_HEAD(WAIT_)                                                                                    \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  WAIT_;                                                                                                     \
+  __builtin_amdgcn_s_barrier();                                                                              \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                         \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  __builtin_amdgcn_s_setprio(1);
+#define IC2_G8_TAIL                                                                                           \
+  __builtin_amdgcn_s_setprio(0);                                                                             \
+  __builtin_amdgcn_sched_barrier(0);                                                                         \
+  __builtin_amdgcn_s_barrier();                                                                              \
+  __builtin_amdgcn_sched_barrier(0);
+#define IC2_G8_MF(qm_, qn_, i_, j_)                                                                           \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + (i_)][(qn_) * 2 + (j_)] =                    \
+      mfma32<F16>(af[i_][s], bfr[j_][s], acc[(qm_) * 4 + (i_)][(qn_) * 2 + (j_)]);
+  // quadrant (qm, qn); the next phase reloads B half nqn of buffer nb: j-major, B fragment group j read behind its MFMAs
+#define IC2_G8_COMPUTE_NB(qm_, qn_, WAIT_, nb_, nqn_)                                                         \
+  IC2_G8_HEAD(WAIT_)                                                                                          \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                            \
+    if ((qm_) == 0 ? live0 : live1) {                                                                        \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) { IC2_G8_MF(qm_, qn_, i, j) }                            \
+    }                                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+    IC2_G8_READ_BJ(nb_, nqn_, j)                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+  }                                                                                                          \
+  IC2_G8_TAIL
+  // ... reloads A half nqm: i-major, A fragment group i read behind its MFMAs; NB_ALSO: then all of B half nqn
+#define IC2_G8_COMPUTE_NA(qm_, qn_, WAIT_, nb_, nqm_, nqn_, NB_ALSO)                                          \
+  IC2_G8_HEAD(WAIT_)                                                                                          \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                            \
+    if ((qm_) == 0 ? live0 : live1) {                                                                        \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) { IC2_G8_MF(qm_, qn_, i, j) }                            \
+    }                                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+    IC2_G8_READ_AI(nb_, nqm_, i)                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+  }                                                                                                          \
+  if (NB_ALSO) {                                                                                             \
+    IC2_G8_READ_B(nb_, nqn_)                                                                                 \
+  }                                                                                                          \
+  IC2_G8_TAIL
+  // phase 0's operands (buf0, retired by the prologue's wait and barrier)
+  IC2_G8_READ_B(0, 0);
+  IC2_G8_READ_A(0, 0);
+  for (int it = 0; it < niter; ++it) {
+    const Cur cA = cn;               // 2i+1
+    const Cur cB = advance(cA);      // 2i+2
+    const Cur cC = advance(cB);      // 2i+3
+    IC2_G8_ISSUE_A(1, 1, cA);                                   // ph0 (0,0); next: B(buf0, 1)
+    IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 0, 1);
+    IC2_G8_ISSUE_B(0, 1, cA);                                   // ph1 (0,1); next: A(buf0, 1)
+    IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 0, 1, 0, false);
+    IC2_G8_ISSUE_A(0, 0, cB);                                   // ph2 (1,1); next: B(buf0, 0)
+    IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 0, 0);
+    IC2_G8_ISSUE_B(1, 0, cB);                                   // ph3 (1,0), retires buf1; next: A, B(buf1, 0)
+    IC2_G8_COMPUTE_NA(1, 0, IC2_G8_WAIT, 1, 0, 0, true);
+    IC2_G8_ISSUE_A(1, 0, cB);                                   // ph4 (0,0); next: B(buf1, 1)
+    IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 1, 1);
+    IC2_G8_ISSUE_B(0, 0, cB);                                   // ph5 (0,1); next: A(buf1, 1)
+    IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 1, 1, 0, false);
+    IC2_G8_ISSUE_A(0, 1, cC);                                   // ph6 (1,1); next: B(buf1, 0)
+    IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 1, 0);
+    IC2_G8_ISSUE_B(1, 1, cC);                                   // ph7 (1,0), retires buf0; next: A, B(buf0, 0)
+    IC2_G8_COMPUTE_NA(1, 0, IC2_G8_WAIT, 0, 0, 0, true);
+    cn = cC;
+  }
+#undef IC2_G8_READ_AI
+#undef IC2_G8_READ_BJ
+#undef IC2_G8_HEAD
+#undef IC2_G8_TAIL
+#undef IC2_G8_MF
+#undef IC2_G8_COMPUTE_NB
+#undef IC2_G8_COMPUTE_NA
+#else
   for (int it = 0; it < niter; ++it) {
     const Cur cA = cn;               // 2i+1
     const Cur cB = advance(cA);      // 2i+2
@@ -552,6 +642,7 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
     IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
     cn = cC;
   }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail DMAs (zero tiles) before exit
   if (half == 0) __builtin_amdgcn_s_barrier();      // balance the waves 4-7 offset barrier
 #undef IC2_G8_ISSUE_A

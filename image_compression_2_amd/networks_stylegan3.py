@@ -481,8 +481,7 @@ class SynthesisLayer(torch.nn.Module):
 
     def packed_adjoint_wino(self, scale=1.0):
         """packed_adjoint for the Winograd kernel: U [cin_p][3][4][cout_p] f16 of the normalised W flipped in space
-        and transposed in channels (ic2_pack_weight_wino on the f32 adjoint, no further normalisation), times `scale`
-        (a power of two: the training dgrad packs 2 U against a halved dc, autograd_ops._synth_layer_grads)."""
+        and transposed in channels (ic2_pack_weight_wino on the f32 adjoint, no further normalisation), times `scale`."""
         key = (_version_key(self.weight), scale)
         hit = self._cache.get(("adj_wino", scale))
         if hit is not None and hit[0] == key:

@@ -5,7 +5,9 @@
 #   bash tools/gpu_evidence.sh <tag> [tests [K] smoke c2 c4 c5 trace trace5 pmc pmc4]   (default: c2 c4 c5 trace pmc)
 # tests: the GPU pytest suite (optionally only `-k K`, K = comma-separated alternatives), smoke: __graft_entry__.smoke(), pmc4: the C4 PMC traffic,
 # abwino <tag>: the Winograd conv of image_compression_2_amd/libic2ops_<tag>.so (tools/build_abl.sh) against the default
-# library -- tests/test_gpu_wino.py on the variant, then tools/bench_wino.py on both, alternating, two rounds.
+# library -- tests/test_gpu_wino.py on the variant, then tools/bench_wino.py on both, alternating, two rounds;
+# ab <tag> <tests> <shapes>: the same for any variant library, <tests> = comma-separated test files under tests/,
+# <shapes> = comma-separated tools/bench_wino.py shapes (its "direct" column times the implicit-GEMM plan).
 # (Replaces the round-5 one-shot gpu_*.sh scripts.)
 set -o pipefail
 cd $GRAFT_REPO_ROOT || exit 1
@@ -26,7 +28,7 @@ while [ $# -gt 0 ]; do
     tests)
       k=""
       # K: a pytest -k expression without spaces, alternatives separated by commas (ddp,wino -> "ddp or wino")
-      if [ $# -gt 0 ] && ! [[ " abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=${1//,/ or }; shift; fi
+      if [ $# -gt 0 ] && ! [[ " ab abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=${1//,/ or }; shift; fi
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${k:+-k "$k"} \
         > $o/${tag}_pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $o/${tag}_pytest.log | tail -30; tail -30 $o/${tag}_pytest.log; exit 1; }
       tail -2 $o/${tag}_pytest.log ;;
@@ -40,6 +42,22 @@ while [ $# -gt 0 ]; do
           IC2_DEV=1 IC2_DEV_LIB=image_compression_2_amd/$lib.so timeout -k 10 300 python -u tools/bench_wino.py s52 s84 s148 s148b s148c \
             > $o/${tag}_ab_${lib}_$rnd.log 2>&1 || { echo "bench_wino failed ($lib)"; tail -20 $o/${tag}_ab_${lib}_$rnd.log; exit 1; }
           echo "== $lib round $rnd"; grep -E "wino" $o/${tag}_ab_${lib}_$rnd.log | tail -6
+        done
+      done ;;
+    ab)
+      v=$1; tf=$2; shp=$3; shift 3
+      files=""; for f in ${tf//,/ }; do files="$files tests/$f"; done
+      IC2_DEV=1 IC2_DEV_LIB=image_compression_2_amd/libic2ops_$v.so timeout -k 10 600 python -u -m pytest $files \
+        -x -q --timeout 200 --timeout-method thread > $o/${tag}_ab_$v.log 2>&1 || { echo "variant tests failed"; tail -30 $o/${tag}_ab_$v.log; exit 1; }
+      tail -1 $o/${tag}_ab_$v.log
+      for rnd in 1 2; do
+        for lib in libic2ops libic2ops_$v; do
+          IC2_DEV=1 IC2_DEV_LIB=image_compression_2_amd/$lib.so timeout -k 10 300 python -u tools/bench_wino.py ${shp//,/ } \
+            > $o/${tag}_ab_${lib}_$rnd.log 2>&1 || { echo "bench_wino failed ($lib)"; tail -20 $o/${tag}_ab_${lib}_$rnd.log; exit 1; }
+          echo "== $lib round $rnd"; cat $o/${tag}_ab_${lib}_$rnd.log | python3 -c "import sys,json
+for l in sys.stdin:
+    n,_,j=l.partition(' ')
+    if j.startswith('{'): d=json.loads(j); print(n, 'direct', d['direct'], 'wino', d['wino'])"
         done
       done ;;
     smoke)
