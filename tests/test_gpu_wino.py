@@ -203,6 +203,8 @@ def test_wino_dgrad_overflows_at_the_direct_gemms_scale(cuda):
             ref = dd[..., :L.in_channels].double()
             err = (dw[..., :L.in_channels].double() - ref).abs().max().item() / ref.abs().max().item()
             assert err < 4e-3, (k, err)
+        if len(first) == 2:
+            break
     print(f"[wino dgrad] first non-finite scale 2^k: {first}")
     assert "direct" in first and first.get("wino") == first["direct"], first
 

@@ -29,7 +29,7 @@ while [ $# -gt 0 ]; do
       k=""
       # K: a pytest -k expression without spaces, alternatives separated by commas (ddp,wino -> "ddp or wino")
       if [ $# -gt 0 ] && ! [[ " ab abwino smoke c2 c4 c5 trace trace5 pmc pmc4 " == *" $1 "* ]]; then k=${1//,/ or }; shift; fi
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${k:+-k "$k"} \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread ${k:+-k "$k"} \
         > $o/${tag}_pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $o/${tag}_pytest.log | tail -30; tail -30 $o/${tag}_pytest.log; exit 1; }
       tail -2 $o/${tag}_pytest.log ;;
     abwino)
