@@ -28,8 +28,9 @@ for abl in "$@"; do
   objs=""
   for f in image_compression_2_amd/csrc/*.hip; do
     o=$d/$(basename $f .hip).o
-    if [ "$(basename $f)" != $src ] && [ ! -f $o ] && [ -f image_compression_2_amd/_build/$(basename $f .hip).o ]; then
-      cp image_compression_2_amd/_build/$(basename $f .hip).o $o   # only $src differs
+    b=image_compression_2_amd/_build/$(basename $f .hip).o
+    if [ "$(basename $f)" != $src ] && [ -f $b ] && { [ ! -f $o ] || [ $b -nt $o ]; }; then
+      cp -p $b $o   # only $src differs (refreshed whenever the default build's object is newer)
     fi
     if [ "$(basename $f)" = $src ] || [ ! -f $o ]; then
       /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Wno-unused-result -D$def=$abl $EXTRA \
