@@ -518,9 +518,10 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   Cur cn = c1;  // tile 2i+1
 #if IC2_G8_PF
   // Prefetch schedule (IC2_G8_PF=1): a phase's new operand is read inside the PREVIOUS phase's MFMA section, each
-  // 16-row fragment group right behind the MFMAs that consumed its registers (no extra registers), so a phase's R
-  // section holds only its DMA issue and waits.  Legal: every half is read >= 0 phases after the vmcnt + barrier
-  // that retires it (buf1 at phase 3, buf0 at phase 7) and >= 2 phases before it is restaged.
+  // 16-row fragment group right behind the MFMAs that consumed its registers (no extra registers), so the R section
+  // holds only the DMA issue and waits -- except at phases 0 and 4, whose buffer is retired by the vmcnt + barrier of
+  // phase 7 / 3: waves 4-7 pass that wait one barrier later, so waves 0-3 may read it only from the next R section.
+  // Every prefetched half is read >= 2 phases before it is restaged.
 #define IC2_G8_READ_AI(buf_, qm_, i_)                                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s) af[i_][s] =                                                  \
       *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + g8_off(grp * 128 + (qm_) * 64 + (i_) * 16 + fr, 4 * s + fh));
@@ -569,29 +570,30 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
     IC2_G8_READ_B(nb_, nqn_)                                                                                 \
   }                                                                                                          \
   IC2_G8_TAIL
-  // phase 0's operands (buf0, retired by the prologue's wait and barrier)
-  IC2_G8_READ_B(0, 0);
-  IC2_G8_READ_A(0, 0);
   for (int it = 0; it < niter; ++it) {
     const Cur cA = cn;               // 2i+1
     const Cur cB = advance(cA);      // 2i+2
     const Cur cC = advance(cB);      // 2i+3
-    IC2_G8_ISSUE_A(1, 1, cA);                                   // ph0 (0,0); next: B(buf0, 1)
+    IC2_G8_READ_B(0, 0);                                        // ph0 (0,0): operands read in R; next: B(buf0, 1)
+    IC2_G8_READ_A(0, 0);
+    IC2_G8_ISSUE_A(1, 1, cA);
     IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 0, 1);
     IC2_G8_ISSUE_B(0, 1, cA);                                   // ph1 (0,1); next: A(buf0, 1)
     IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 0, 1, 0, false);
     IC2_G8_ISSUE_A(0, 0, cB);                                   // ph2 (1,1); next: B(buf0, 0)
     IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 0, 0);
-    IC2_G8_ISSUE_B(1, 0, cB);                                   // ph3 (1,0), retires buf1; next: A, B(buf1, 0)
-    IC2_G8_COMPUTE_NA(1, 0, IC2_G8_WAIT, 1, 0, 0, true);
-    IC2_G8_ISSUE_A(1, 0, cB);                                   // ph4 (0,0); next: B(buf1, 1)
+    IC2_G8_ISSUE_B(1, 0, cB);                                   // ph3 (1,0), retires buf1
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
+    IC2_G8_READ_B(1, 0);                                        // ph4 (0,0): operands read in R; next: B(buf1, 1)
+    IC2_G8_READ_A(1, 0);
+    IC2_G8_ISSUE_A(1, 0, cB);
     IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 1, 1);
     IC2_G8_ISSUE_B(0, 0, cB);                                   // ph5 (0,1); next: A(buf1, 1)
     IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 1, 1, 0, false);
     IC2_G8_ISSUE_A(0, 1, cC);                                   // ph6 (1,1); next: B(buf1, 0)
     IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 1, 0);
-    IC2_G8_ISSUE_B(1, 1, cC);                                   // ph7 (1,0), retires buf0; next: A, B(buf0, 0)
-    IC2_G8_COMPUTE_NA(1, 0, IC2_G8_WAIT, 0, 0, 0, true);
+    IC2_G8_ISSUE_B(1, 1, cC);                                   // ph7 (1,0), retires buf0
+    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
     cn = cC;
   }
 #undef IC2_G8_READ_AI
