@@ -323,10 +323,6 @@ __device__ __forceinline__ int g8_off(int row, int chunk) { return row * 128 + (
 __device__ __forceinline__ int g8_arow(int qm, int g, int l) { return (g >> 3) * 128 + qm * 64 + (g & 7) * 8 + l; }
 __device__ __forceinline__ int g8_brow(int qn, int g, int l) { return (g >> 2) * 64 + qn * 32 + (g & 3) * 8 + l; }
 
-// IC2_G8_PF=1 (A/B build): the prefetch schedule (below); 0: fragments read in the phase that uses them
-#ifndef IC2_G8_PF
-#define IC2_G8_PF 0
-#endif
 template <int OG, bool F16 = false>
 __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   using G = G8<OG>;
@@ -516,94 +512,6 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
 
   const int niter = (t_end - t_begin + 1) >> 1;
   Cur cn = c1;  // tile 2i+1
-#if IC2_G8_PF
-  // Prefetch schedule (IC2_G8_PF=1): a phase's new operand is read inside the PREVIOUS phase's MFMA section, each
-  // 16-row fragment group right behind the MFMAs that consumed its registers (no extra registers), so the R section
-  // holds only the DMA issue and waits -- except at phases 0 and 4, whose buffer is retired by the vmcnt + barrier of
-  // phase 7 / 3: waves 4-7 pass that wait one barrier later, so waves 0-3 may read it only from the next R section.
-  // Every prefetched half is read >= 2 phases before it is restaged.
-#define IC2_G8_READ_AI(buf_, qm_, i_)                                                                         \
-  _Pragma("unroll") for (int s = 0; s < 2; ++s) af[i_][s] =                                                  \
-      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + g8_off(grp * 128 + (qm_) * 64 + (i_) * 16 + fr, 4 * s + fh));
-#define IC2_G8_READ_BJ(buf_, qn_, j_)                                                                         \
-  _Pragma("unroll") for (int s = 0; s < 2; ++s) bfr[j_][s] =                                                 \
-      *reinterpret_cast<const bf16x8*>(lds + (buf_) * G::BUF + G::BOFF + g8_off(wp_ * 64 + (qn_) * 32 + (j_) * 16 + fr, 4 * s + fh));
-#define IC2_G8_HEAD(WAIT_)                                                                                    \
-  __builtin_amdgcn_sched_barrier(0);                                                                         \
-  WAIT_;                                                                                                     \
-  __builtin_amdgcn_s_barrier();                                                                              \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                         \
-  __builtin_amdgcn_sched_barrier(0);                                                                         \
-  __builtin_amdgcn_s_setprio(1);
-#define IC2_G8_TAIL                                                                                           \
-  __builtin_amdgcn_s_setprio(0);                                                                             \
-  __builtin_amdgcn_sched_barrier(0);                                                                         \
-  __builtin_amdgcn_s_barrier();                                                                              \
-  __builtin_amdgcn_sched_barrier(0);
-#define IC2_G8_MF(qm_, qn_, i_, j_)                                                                           \
-  _Pragma("unroll") for (int s = 0; s < 2; ++s) acc[(qm_) * 4 + (i_)][(qn_) * 2 + (j_)] =                    \
-      mfma32<F16>(af[i_][s], bfr[j_][s], acc[(qm_) * 4 + (i_)][(qn_) * 2 + (j_)]);
-  // quadrant (qm, qn); the next phase reloads B half nqn of buffer nb: j-major, B fragment group j read behind its MFMAs
-#define IC2_G8_COMPUTE_NB(qm_, qn_, WAIT_, nb_, nqn_)                                                         \
-  IC2_G8_HEAD(WAIT_)                                                                                          \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                            \
-    if ((qm_) == 0 ? live0 : live1) {                                                                        \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i) { IC2_G8_MF(qm_, qn_, i, j) }                            \
-    }                                                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                                                       \
-    IC2_G8_READ_BJ(nb_, nqn_, j)                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                                                       \
-  }                                                                                                          \
-  IC2_G8_TAIL
-  // ... reloads A half nqm: i-major, A fragment group i read behind its MFMAs; NB_ALSO: then all of B half nqn
-#define IC2_G8_COMPUTE_NA(qm_, qn_, WAIT_, nb_, nqm_, nqn_, NB_ALSO)                                          \
-  IC2_G8_HEAD(WAIT_)                                                                                          \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                            \
-    if ((qm_) == 0 ? live0 : live1) {                                                                        \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j) { IC2_G8_MF(qm_, qn_, i, j) }                            \
-    }                                                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                                                       \
-    IC2_G8_READ_AI(nb_, nqm_, i)                                                                             \
-    __builtin_amdgcn_sched_barrier(0);                                                                       \
-  }                                                                                                          \
-  if (NB_ALSO) {                                                                                             \
-    IC2_G8_READ_B(nb_, nqn_)                                                                                 \
-  }                                                                                                          \
-  IC2_G8_TAIL
-  for (int it = 0; it < niter; ++it) {
-    const Cur cA = cn;               // 2i+1
-    const Cur cB = advance(cA);      // 2i+2
-    const Cur cC = advance(cB);      // 2i+3
-    IC2_G8_READ_B(0, 0);                                        // ph0 (0,0): operands read in R; next: B(buf0, 1)
-    IC2_G8_READ_A(0, 0);
-    IC2_G8_ISSUE_A(1, 1, cA);
-    IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 0, 1);
-    IC2_G8_ISSUE_B(0, 1, cA);                                   // ph1 (0,1); next: A(buf0, 1)
-    IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 0, 1, 0, false);
-    IC2_G8_ISSUE_A(0, 0, cB);                                   // ph2 (1,1); next: B(buf0, 0)
-    IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 0, 0);
-    IC2_G8_ISSUE_B(1, 0, cB);                                   // ph3 (1,0), retires buf1
-    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
-    IC2_G8_READ_B(1, 0);                                        // ph4 (0,0): operands read in R; next: B(buf1, 1)
-    IC2_G8_READ_A(1, 0);
-    IC2_G8_ISSUE_A(1, 0, cB);
-    IC2_G8_COMPUTE_NB(0, 0, IC2_G8_NOWAIT, 1, 1);
-    IC2_G8_ISSUE_B(0, 0, cB);                                   // ph5 (0,1); next: A(buf1, 1)
-    IC2_G8_COMPUTE_NA(0, 1, IC2_G8_NOWAIT, 1, 1, 0, false);
-    IC2_G8_ISSUE_A(0, 1, cC);                                   // ph6 (1,1); next: B(buf1, 0)
-    IC2_G8_COMPUTE_NB(1, 1, IC2_G8_NOWAIT, 1, 0);
-    IC2_G8_ISSUE_B(1, 1, cC);                                   // ph7 (1,0), retires buf0
-    IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
-    cn = cC;
-  }
-#undef IC2_G8_READ_AI
-#undef IC2_G8_READ_BJ
-#undef IC2_G8_HEAD
-#undef IC2_G8_TAIL
-#undef IC2_G8_MF
-#undef IC2_G8_COMPUTE_NB
-#undef IC2_G8_COMPUTE_NA
-#else
   for (int it = 0; it < niter; ++it) {
     const Cur cA = cn;               // 2i+1
     const Cur cB = advance(cA);      // 2i+2
@@ -644,7 +552,6 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
     IC2_G8_COMPUTE(1, 0, IC2_G8_WAIT);
     cn = cC;
   }
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail DMAs (zero tiles) before exit
   if (half == 0) __builtin_amdgcn_s_barrier();      // balance the waves 4-7 offset barrier
 #undef IC2_G8_ISSUE_A
@@ -1228,7 +1135,15 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     int g8_split = 1;
     // knob IC2_G8_TARGET: workgroups the split aims at (default 240, ~1 per CU of the 1-workgroup-per-CU kernel)
     static const int g8_target = knob("IC2_G8_TARGET", 240);
-    if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) tile = 6;
+    // wave balance (knob IC2_G8_BALANCE): a full-K grid of 1-2 rounds whose last round leaves most CUs idle (SG3-T-256
+    // L0-L3: 362 workgroups = 1.41 rounds on 256 CUs) splits K in two (2.83 rounds), when that fills the rounds
+    // >= 15 points better
+    static const bool g8_balance = knob("IC2_G8_BALANCE", 1) != 0;
+    auto fill = [](int64_t wg) { return (double)wg / (256.0 * (double)ceil_div(wg, 256)); };
+    if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) {
+      tile = 6;
+      if (g8_balance && splitk && g8_splitk && g6 < 512 && K / 64 >= 16 && fill(2 * g6) > fill(g6) + 0.15) g8_split = 2;
+    }
     else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) && g7 >= 240) tile = 7;
     else if (g8_splitk && splitk && fits8 && k_deep && cout_p > 128 && !odd128)
       tile = 6, g8_split = (int)ceil_div(g8_target, g6);

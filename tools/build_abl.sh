@@ -7,12 +7,11 @@
 #   bash tools/build_abl.sh winosched 1 2   IC2_WX_SCHED schedule variants  -> libic2ops_wxsched<N>.so
 #   bash tools/build_abl.sh winoprio 1 2    IC2_WX_PRIO wave-priority variants -> libic2ops_wxprio<N>.so
 #   bash tools/build_abl.sh hg4pair 0       IC2_HG4_PAIR=0: split-weight f16 hg4 in the plain K order -> libic2ops_hg4pair0.so
-#   bash tools/build_abl.sh g8pf 1          IC2_G8_PF=1: the 8-phase conv's prefetch schedule -> libic2ops_g8pf1.so
 #   (EXTRA="-DIC2_WX_SCHED=2" bash tools/build_abl.sh winostamp 1: stamps of a variant)
 set -e
 cd "$(dirname "$0")/.."
 kind=flr
-if [ "$1" = flr ] || [ "$1" = hg4 ] || [ "$1" = wino ] || [ "$1" = winostamp ] || [ "$1" = winosched ] || [ "$1" = winoprio ] || [ "$1" = hg4pair ] || [ "$1" = g8pf ]; then
+if [ "$1" = flr ] || [ "$1" = hg4 ] || [ "$1" = wino ] || [ "$1" = winostamp ] || [ "$1" = winosched ] || [ "$1" = winoprio ] || [ "$1" = hg4pair ]; then
   kind=$1; shift
 fi
 if [ $kind = flr ]; then src=flrelu_mfma.hip; def=IC2_FM3_ABL; tag=abl;
@@ -21,7 +20,6 @@ elif [ $kind = winostamp ]; then src=wino.hip; def=IC2_WX_STAMP; tag=wxstamp;
 elif [ $kind = winosched ]; then src=wino.hip; def=IC2_WX_SCHED; tag=wxsched;
 elif [ $kind = winoprio ]; then src=wino.hip; def=IC2_WX_PRIO; tag=wxprio;
 elif [ $kind = hg4pair ]; then src=igemm.hip; def=IC2_HG4_PAIR; tag=hg4pair;
-elif [ $kind = g8pf ]; then src=igemm.hip; def=IC2_G8_PF; tag=g8pf;
 else src=igemm.hip; def=IC2_HG4_ABL; tag=hg4abl; fi
 for abl in "$@"; do
   d=image_compression_2_amd/_build_$tag$abl; mkdir -p $d
