@@ -77,10 +77,9 @@ __device__ __forceinline__ int wx_hoff(int line, int hp, int idx, int chunk) {
 #define IC2_WX_STAMP 0
 #endif
 // schedule variants (A/B): 0 = reads, V, then DMAs in R; 1 = DMAs first in R; 2 = DMAs first, and the next step's
-// input fragments read inside the second M section of the step (halo DMAs one section later to keep the WAR distance);
-// 3 = the next section's A fragments read inside this section's M, each half right behind the 8 MFMAs that consumed
-// its registers (R keeps only the V / input work, the DMAs and the waits; no extra registers); 5 = 3, and the next
-// step's input fragments read inside the step's first M section, between its two MFMA halves (R holds no LDS read)
+// input fragments read inside the second M section of the step (halo DMAs one section later to keep the WAR distance).
+// (Round 6 also tried the next section's A fragments read inside this section's M section, right behind the MFMAs that
+// consumed their registers, with and without the input fragments: level / 2-3 % slower, profiles/r6_schedule_ab.txt.)
 #ifndef IC2_WX_SCHED
 #define IC2_WX_SCHED 0
 #endif
@@ -244,11 +243,6 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[nl][i] = *reinterpret_cast<const bf16x8*>(wl + (nl * 64 + i * 16) * 64);
   };
-  if constexpr (IC2_WX_SCHED == 3 || IC2_WX_SCHED == 5) {  // section 0's A fragments (half-slabs 0-2 landed before
-                                                           // the barrier above)
-    read_a(wsl + aoff, 0);
-    read_a(wsl + aoff, 1);
-  }
   if (half == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 run one barrier behind
   __builtin_amdgcn_sched_barrier(0);
 
@@ -269,8 +263,6 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
     for (int j = 0; j < 6; ++j) {
       const int ky = j >> 1, hx = j & 1;
       const char* wl = wsl + j * (WX_SLAB / 2) + aoff;
-      // the next section's half-slab: ring slot (j + 1) % 6 (past the last section: a slot's stale bytes, unused)
-      const char* wl_next = wsl + (j == 5 ? 0 : (j + 1) * (WX_SLAB / 2)) + aoff;
       // ---- R section
       auto r_dma = [&]() {
         if (!(IC2_WX_ABL & 1) || cb == 0) issue_hs(cb + (j + 5) / 6, (j + 5) % 6);
@@ -286,11 +278,9 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
       if constexpr (IC2_WX_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       if constexpr (IC2_WX_SCHED >= 1) r_dma();
       if (hx == 0) make_v();
-      if constexpr (IC2_WX_SCHED != 3 && IC2_WX_SCHED != 5) {
-        read_a(wl, 0);
-        read_a(wl, 1);
-      }
-      if (hx == 1 && (IC2_WX_SCHED < 2 || IC2_WX_SCHED == 3)) {
+      read_a(wl, 0);
+      read_a(wl, 1);
+      if (hx == 1 && IC2_WX_SCHED < 2) {
         if constexpr (!(IC2_WX_ABL & 4)) read_d(ky < 2 ? hb_cur + (ky + 1) * ky_step : hb_nxt);
       }
       if constexpr (IC2_WX_STAMP) {
@@ -335,12 +325,6 @@ __global__ void __launch_bounds__(512, 1) wino_fx_f16_kernel(IgemmArgs a) {
         if (IC2_WX_SCHED == 2 && hx == 1 && nl == 0) {  // the next step's input fragments behind the MFMAs
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (!(IC2_WX_ABL & 4)) read_d(ky < 2 ? hb_cur + (ky + 1) * ky_step : hb_nxt);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (IC2_WX_SCHED == 3 || IC2_WX_SCHED == 5) {  // this half's registers are free: the next
-          __builtin_amdgcn_sched_barrier(0);                          // section's fragments
-          read_a(wl_next, nl);
-          if (IC2_WX_SCHED == 5 && hx == 0 && nl == 0) read_d(ky < 2 ? hb_cur + (ky + 1) * ky_step : hb_nxt);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
