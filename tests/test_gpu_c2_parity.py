@@ -50,7 +50,7 @@ SNR_FLOOR_E2E = 38.0    # dB, benched encode + quantize + synthesis vs the refer
 PSNR_TOL = 0.005        # dB at the 34 dB operating point, end to end (north star: 0.01)
 PSNR_TOL_46 = 0.01      # dB at 46 dB
 IDX_COUNT_BENCH = 69    # index mismatches of the benched mode at round 5 (BENCH_r05 parity): a ceiling, not a target
-IDX_COUNT_FP32 = 16     # the fp32 parity mode's count on this batch
+IDX_COUNT_FP32 = 4      # the fp32 parity mode: measured 2 on this batch (round 6)
 SNR_FLOOR_F16 = 52.0    # dB, the f16 synthesis (bench --precision f16) vs the fp32 reference (CPU emulation: 60.5)
 
 
