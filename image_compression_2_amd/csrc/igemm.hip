@@ -1135,15 +1135,9 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     int g8_split = 1;
     // knob IC2_G8_TARGET: workgroups the split aims at (default 240, ~1 per CU of the 1-workgroup-per-CU kernel)
     static const int g8_target = knob("IC2_G8_TARGET", 240);
-    // wave balance (knob IC2_G8_BALANCE): a full-K grid of 1-2 rounds whose last round leaves most CUs idle (SG3-T-256
-    // L0-L3: 362 workgroups = 1.41 rounds on 256 CUs) splits K in two (2.83 rounds), when that fills the rounds
-    // >= 15 points better
-    static const bool g8_balance = knob("IC2_G8_BALANCE", 1) != 0;
-    auto fill = [](int64_t wg) { return (double)wg / (256.0 * (double)ceil_div(wg, 256)); };
-    if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) {
-      tile = 6;
-      if (g8_balance && splitk && g8_splitk && g6 < 512 && K / 64 >= 16 && fill(2 * g6) > fill(g6) + 0.15) g8_split = 2;
-    }
+    // (a full-K grid of 1-2 rounds is not split for wave balance: SG3-T-256 L0-L3's 362 workgroups as 724 half-K ones
+    // measured 10 % slower, the f32 partials and the combine costing more than the idle tail, r6_schedule_ab.txt)
+    if (fits8 && cout_p > 128 && !odd128 && g6 >= 240) tile = 6;
     else if (g8n && fits8 && (odd128 || (cout_p > 64 && cout_p <= 128)) && g7 >= 240) tile = 7;
     else if (g8_splitk && splitk && fits8 && k_deep && cout_p > 128 && !odd128)
       tile = 6, g8_split = (int)ceil_div(g8_target, g6);
