@@ -336,6 +336,39 @@ def test_grad_reducer_overlaps_at_c5_config(tmp_path):
             assert steps[step]["launched"] == steps[step]["nb"] == res[0]["n_buckets"], steps[step]["launched"]
 
 
+def _order_worker(out_path):
+    import torch.distributed as dist
+    rank, world, _ = icd.init("gloo")
+    torch.manual_seed(0)
+    m = _ToyEncoder()
+    r = icd.GradReducer(m, world, bucket_bytes=64)
+    x = torch.randn(5, 6, generator=torch.Generator().manual_seed(rank))
+    m.zero_grad(set_to_none=True)
+    r.start()
+    m(x).sum().backward()
+    if rank == 1:
+        r._fired.reverse()   # a rank whose hooks fired in another order (the rebuild must not trust it)
+    r.finish()
+    names = {id(p): k for k, p in m.named_parameters()}
+    names.update({id(p): f"param{i}" for i, p in enumerate(r.params) if id(p) not in names})
+    torch.save({"buckets": [[names[id(p)] for p in b] for b in r.buckets]}, f"{out_path}.{rank}")
+    r.remove()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_rebuild_uses_rank0_order(tmp_path):
+    """The rebuilt buckets come from rank 0's recorded hook order on every rank (broadcast), so ranks whose hooks fired
+    in different orders still issue the same collective sequence; the parameter without a gradient is left out."""
+    out = str(tmp_path / "ord")
+    icd.launch(2, _order_worker, out)
+    r0, r1 = (torch.load(f"{out}.{r}", weights_only=True) for r in range(2))
+    assert r0["buckets"] == r1["buckets"] and r0["buckets"]
+    flat = [k for b in r0["buckets"] for k in b]
+    assert "unused" not in flat and len(flat) == len(set(flat))
+    assert {"a.weight", "a.bias", "b.weight", "b.bias"} <= set(flat)
+
+
 def test_grad_reducer_single_process_is_inert():
     m = _ToyEncoder()
     r = icd.GradReducer(m, world=1)
