@@ -2,7 +2,7 @@
 bench's C5 setup (f16 + loss scaler), counted per op name and, where the profiler recorded a Python stack, the
 innermost package frame (ops issued from the autograd engine's backward thread carry none: "?").
 
-    python tools/prof_c5_ops.py [--steps 2] [--top 40]
+    python tools/prof_c5_ops.py [--steps 2] [--top 40] [--mode profiler|dispatch]
 """
 import argparse
 import os
@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--mode", choices=("profiler", "dispatch"), default="profiler")
     args = ap.parse_args()
     import image_compression_2_amd as ic2
     from image_compression_2_amd import training as ict
@@ -38,6 +39,36 @@ def main():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    if args.mode == "dispatch":
+        # TorchDispatchMode census: every ATen op that reaches the backend, attributed to the innermost package frame
+        # of the Python stack of the thread that issued it (the autograd engine runs the package's Function.backward in
+        # Python, so its ops carry their frame too)
+        import traceback
+        from torch.utils._python_dispatch import TorchDispatchMode
+        counts = {}
+
+        class Census(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args_=(), kwargs=None):
+                fr = "?"
+                for f in reversed(traceback.extract_stack()[:-1]):
+                    if "image_compression_2_amd" in f.filename or "torch/amp" in f.filename or "torch/optim" in f.filename:
+                        fr = f"{os.path.basename(f.filename)}:{f.lineno}"
+                        break
+                key = (str(func.overloadpacket.__name__), fr)
+                counts[key] = counts.get(key, 0) + 1
+                return func(*args_, **(kwargs or {}))
+        with Census():
+            for _ in range(args.steps):
+                step()
+        torch.cuda.synchronize()
+        skip = {"view", "_unsafe_view", "as_strided", "detach", "t", "transpose", "permute", "expand", "slice", "select",
+                "unsqueeze", "squeeze", "reshape", "alias", "split", "chunk", "unbind", "empty", "empty_like",
+                "empty_strided", "is_same_size", "_to_copy_view", "lift_fresh"}
+        rows = [(k, c) for k, c in counts.items() if k[0] not in skip]
+        print(f"ops per step (views / empties excluded): {sum(c for _, c in rows) / args.steps:.0f}")
+        for (name, frame), c in sorted(rows, key=lambda kv: -kv[1])[: args.top]:
+            print(f"{c / args.steps:7.1f}  {name:32s} {frame}")
+        return
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         for _ in range(args.steps):
