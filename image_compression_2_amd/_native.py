@@ -58,6 +58,7 @@ _SIGS = {
     "ic2_conv_igemm_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F,
                           _I, _P, _I64, _P],
     "ic2_pack_weight_wino": [_P, _I, _I, _I, _I, _I, _F, _P, _I, _P],
+    "ic2_pack_weight_adjoint": [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P],
     "ic2_conv_wino": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I, _P],
     "ic2_conv_wino_plan": [_I, _I, _I, _I, _I, _I],
     "ic2_conv_wino_preferred": [_I, _I, _I, _I, _I, _I, _I, _I, _I],

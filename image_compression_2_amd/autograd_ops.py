@@ -38,6 +38,17 @@ def _pad_to(c_p, t):
     return t if t.shape[-1] == c_p else torch.nn.functional.pad(t, (0, c_p - t.shape[-1]))
 
 
+def pack_conv_weight_adjoint(weight, cout_p, cin_p, dt):
+    """[cout][cin][kh][kw] f32 -> the dgrad pack [cin_p][kh][kw][cout_p] (dt): W flipped in space and transposed in
+    channels, gathered in one launch (ic2_pack_weight_adjoint)."""
+    w = weight.detach().to(torch.float32).contiguous()
+    cout, cin, kh, kw = w.shape
+    out = torch.empty([cin_p, kh, kw, cout_p], dtype=dt, device=w.device)
+    nv.call("ic2_pack_weight_adjoint", nv.ptr(w), cout, cin, kh, kw, cin_p, cout_p, nv.ptr(out), nv.dtype_code(dt),
+            nv.stream_of(w))
+    return out
+
+
 def pack_conv_weight(weight, cin_p, cout_p, dt):
     """[cout][cin][kh][kw] f32 -> packed [cout_p][kh][kw][cin_p] (dt) on the device."""
     w = weight.detach().to(torch.float32).contiguous()
@@ -153,7 +164,7 @@ class Conv2dNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # dx = conv(dy, W flipped in space, transposed in channels), padding k - 1 - pad
             wtp = _derived(ctx.weight, ("adj", cin_p, cout_p, x.dtype),
-                           lambda: pack_conv_weight(weight.detach().transpose(0, 1).flip(2, 3), cout_p, cin_p, x.dtype))
+                           lambda: pack_conv_weight_adjoint(weight, cout_p, cin_p, x.dtype))
             dx = conv_nhwc(dy, wtp, None, cin_p, kh, kh - 1 - ctx.pad, grad=True)
         if ctx.needs_input_grad[1]:
             nfl = int(nv.query("ic2_conv_wgrad_ws_floats", n, h, w, cin_p, cout_p, kh, kw, ctx.pad))

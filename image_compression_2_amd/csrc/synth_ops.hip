@@ -501,6 +501,43 @@ extern "C" int ic2_fc(const float* x, int64_t ldx, const float* w, const float* 
   return IC2_OK;
 }
 
+// the adjoint (dgrad) pack of w[cout][cin][kh][kw]: out[ci][ky][kx][co] = w[co][ci][kh-1-ky][kw-1-kx], zero padded to
+// [cin_p][kh][kw][cout_p] -- W flipped in space and transposed in channels, gathered straight from the parameter (the
+// torch transpose / flip / contiguous it replaces cost two extra launches per conv and training step)
+template <typename T>
+__global__ void __launch_bounds__(256) pack_adjoint_kernel(const float* __restrict__ w, int cout, int cin, int kh,
+                                                           int kw, int cin_p, int cout_p, T* __restrict__ out) {
+  const int ci = blockIdx.x;  // the adjoint conv's output channel
+  const int kk = kh * kw;
+  const int total = kk * cout_p;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int co = e % cout_p, k = e / cout_p;
+    float v = 0.f;
+    if (ci < cin && co < cout) v = w[((int64_t)co * cin + ci) * kk + (kk - 1 - k)];
+    st(out + (int64_t)ci * total + e, v);
+  }
+}
+
+extern "C" int ic2_pack_weight_adjoint(const float* w, int cout, int cin, int kh, int kw, int cin_p, int cout_p,
+                                       void* w_out, int dtype, void* stream) {
+  IC2_CHECK_ARG(w && w_out && cout > 0 && cin > 0 && kh > 0 && kw > 0 && cout_p >= cout && cin_p >= cin,
+                "pack_weight_adjoint: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (dtype == IC2_F32)
+    hipLaunchKernelGGL(pack_adjoint_kernel<float>, dim3(cin_p), dim3(256), 0, s, w, cout, cin, kh, kw, cin_p, cout_p,
+                       (float*)w_out);
+  else if (dtype == IC2_BF16)
+    hipLaunchKernelGGL(pack_adjoint_kernel<bf16_t>, dim3(cin_p), dim3(256), 0, s, w, cout, cin, kh, kw, cin_p, cout_p,
+                       (bf16_t*)w_out);
+  else if (dtype == IC2_F16)
+    hipLaunchKernelGGL(pack_adjoint_kernel<_Float16>, dim3(cin_p), dim3(256), 0, s, w, cout, cin, kh, kw, cin_p, cout_p,
+                       (_Float16*)w_out);
+  else
+    IC2_CHECK_ARG(false, "pack_weight_adjoint: bad dtype %d", dtype);
+  IC2_CHECK_LAUNCH("pack_weight_adjoint");
+  return IC2_OK;
+}
+
 extern "C" int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
                                float scale, void* w_out, int dtype, float* wsq_out, void* stream) {
   IC2_CHECK_ARG(w && w_out && cout > 0 && cin > 0 && kh > 0 && kw > 0 && cout_p >= cout && cin_p >= cin,

@@ -155,6 +155,13 @@ int ic2_fc(const float* x, int64_t ldx, const float* w, const float* b, float* y
 int ic2_pack_weight(const float* w, int cout, int cin, int kh, int kw, int cout_p, int cin_p, int prenorm,
                     float scale, void* w_out, int dtype, float* wsq_out, void* stream);
 
+/* The dgrad pack of the same weight (training; replaces ic2_pack_weight on w.transpose(0, 1).flip(2, 3)):
+ * w[cout][cin][kh][kw] f32 -> w_out[cin_p][kh][kw][cout_p] (IC2_F32 / IC2_BF16 / IC2_F16), w_out[ci][ky][kx][co] =
+ * w[co][ci][kh-1-ky][kw-1-kx], zero padded.  The forward conv (ic2_conv_igemm) on it with padding k - 1 - pad is the
+ * adjoint of nn.Conv2d's. */
+int ic2_pack_weight_adjoint(const float* w, int cout, int cin, int kh, int kw, int cin_p, int cout_p, void* w_out,
+                            int dtype, void* stream);
+
 /* modulated_conv2d's modulation/demodulation coefficients [SG3-public], as the equivalent
  * activation-scaling form y[n,o] = oscale[n,o] * sum_{i,k} w_norm[o,i,k] * (xscale[n,i] * x[n,i]):
  *   demod:  s' = s * rsqrt(mean(s^2)) (batch-global), xscale = s',

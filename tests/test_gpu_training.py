@@ -181,6 +181,21 @@ def test_group_norm_backward_kernel(cuda, n, c, groups, h, w, pool, dtype):
 
 
 # ================================================================ synthesis backward (the frozen generator)
+@pytest.mark.parametrize("cout,cin,k,dt", [(64, 32, 3, torch.float16), (130, 96, 3, torch.bfloat16),
+                                            (40, 3, 3, torch.float32), (16, 24, 1, torch.float16)])
+def test_pack_weight_adjoint_equals_flip_transpose_pack(cuda, cout, cin, k, dt):
+    """ic2_pack_weight_adjoint (the dgrad pack gathered in one launch) equals ic2_pack_weight on the torch-flipped,
+    channel-transposed weight, bit for bit, padding included."""
+    w = torch.randn(cout, cin, k, k, device=cuda, generator=torch.Generator(device=cuda).manual_seed(cout + cin))
+    cout_p, cin_p = nv.pad32(cout), nv.pad32(cin)
+    got = ao.pack_conv_weight_adjoint(w, cout_p, cin_p, dt)
+    ref = ao.pack_conv_weight(w.transpose(0, 1).flip(2, 3), cout_p, cin_p, dt)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (cin_p, k, k, cout_p)
+    assert torch.equal(got.view(torch.int16) if dt != torch.float32 else got,
+                       ref.view(torch.int16) if dt != torch.float32 else ref)
+
+
 from image_compression_2_amd import sg3_ops  # noqa: E402
 from image_compression_2_amd import training as ict  # noqa: E402
 from oracle import sg3  # noqa: E402
