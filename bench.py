@@ -489,7 +489,11 @@ def record_summary(vec, n_codes=N_CODES):
 
 def run(args):
     dry = args.dry_run
-    rank, world, local = icd.init("gloo" if dry else None)
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, collectives over gloo (not a measurement)
+    share = os.environ.get("IC2_BENCH_SHARE_GPU") == "1"
+    rank, world, local = icd.init("gloo" if dry or share else None)
+    if share:
+        local = 0
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     res, gen_res, batch, desc = CONFIGS[args.config]
