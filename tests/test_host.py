@@ -32,6 +32,14 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert lib.ic2_abi_version() == 1
 
 
+def test_integration_index_lists_every_entry_point():
+    """INTEGRATION.md's entry-point index names every function the header declares (`x`(`_floats`) names both)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    doc = re.sub(r"`(ic2_\w+)`\(`(_\w+)`\)", lambda m: f"`{m.group(1)}` `{m.group(1)}{m.group(2)}`", doc)
+    listed = set(re.findall(r"`(ic2_[a-z0-9_]+)`", doc))
+    assert [s for s in _declared_symbols() if s not in listed] == []
+
+
 def test_argument_errors_are_reported_without_a_gpu():
     """Validation happens before any launch: a bad call returns IC2_E_INVALID with a message."""
     lib = nv.load()
