@@ -325,7 +325,7 @@ def plan_kernel_tags(plan):
     if p.startswith("igemm8_og2+og1"):
         return ["igemm8_og2", "igemm8_og1"]
     if p.startswith("igemm8_"):
-        return [p.replace("_splitk", "")]
+        return [p.replace("_splitk", "").replace("_tail", "")]
     if p.startswith("igemm_"):
         return ["igemm_kernel"]
     if p.startswith("hg4_"):

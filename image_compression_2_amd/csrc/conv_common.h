@@ -37,6 +37,7 @@ struct IgemmArgs {
   int group;    // p-tiles per o-sweep (tile_coords)
   int korder;   // 8-phase kernels: 0 = tap-major K, 1 = channel-major K (taps innermost)
   int o_base;   // 8-phase kernels: first output channel of this launch (a cout_p split over two tile shapes)
+  int tile_base;  // 8-phase kernels: first logical tile of this launch (the split tail of a grid, see ig_plan)
   int act;
   float slope, act_gain, clamp, out_mul;
   int out_layout, out_dtype;

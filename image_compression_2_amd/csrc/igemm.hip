@@ -277,14 +277,15 @@ __global__ void __launch_bounds__(64 * WGO * WGP, 1) igemm_kernel(IgemmArgs a) {
 
 // split-K combine: sum the slices in slice order (deterministic), then the epilogue; one thread per
 // (pixel, 4 channels)
-__global__ void __launch_bounds__(256) igemm_splitk_reduce_kernel(IgemmArgs a, int splits) {
+__global__ void __launch_bounds__(256) igemm_splitk_reduce_kernel(IgemmArgs a, int splits, int p_lo) {
   const int c4 = a.cout_p >> 2;
-  const int total = a.M * c4;  // < 2^31 (checked by the launcher)
+  const int total = (a.M - p_lo) * c4;  // < 2^31 (checked by the launcher); pixels [p_lo, M) (the split tail)
   const int hw = a.ho * a.wo;
   const int64_t slice = (int64_t)a.M * a.cout_p;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
-    const int p = e / c4;
-    const int ob = (e - p * c4) * 4;
+    const int q = e / c4;
+    const int p = p_lo + q;
+    const int ob = (e - q * c4) * 4;
     const float* src = a.ws + (int64_t)p * a.cout_p + ob;
     f32x4 s = *reinterpret_cast<const f32x4*>(src);
     for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(src + k * slice);
@@ -334,7 +335,8 @@ __device__ __forceinline__ void igemm8_body(const IgemmArgs& a) {
   const int half = wid_u >> 2;                     // waves 4-7 run one barrier behind waves 0-3
   const int grp = OG == 2 ? half : 0;              // o-group
   const int wp_ = OG == 2 ? (wid_u & 3) : wid_u;   // p-group (64 pixels)
-  const int logical = xcd_remap(blockIdx.x, a.nblocks);
+  // a launch may cover logical tiles [tile_base, tile_base + gridDim.x) of the a.nblocks-tile grid (the split tail)
+  const int logical = a.tile_base + xcd_remap(blockIdx.x, gridDim.x);
   int o_tile, p_tile;
   tile_coords(logical, a.tiles_o, a.nblocks / a.tiles_o, a.group, o_tile, p_tile);
   const int o0 = a.o_base + o_tile * G::BO;  // o_base: a launch covering output channels [o_base, ...) only
@@ -578,16 +580,20 @@ static void launch_igemm(IgemmArgs a, int splits, hipStream_t s) {
                      dim3(64 * WGO * WGP), 0, s, a);
 }
 
+// tiles [tile_base, tile_base + ntiles) of the grid (ntiles < 0: all of it from tile_base)
 template <int OG, bool F16 = false>
-static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1, int splits = 1) {
+static void launch_g8(IgemmArgs a, hipStream_t s, int o_base = 0, int o_end = -1, int splits = 1, int tile_base = 0,
+                      int ntiles = -1) {
   a.o_base = o_base;
   a.tiles_o = ((o_end < 0 ? a.cout_p : o_end) - o_base + G8<OG>::BO - 1) / G8<OG>::BO;
   a.nq = a.K / 64;
   a.nblocks = (int)(ceil_div(a.M, G8<OG>::BP) * a.tiles_o);
+  a.tile_base = tile_base;
+  const unsigned grid = (unsigned)(ntiles < 0 ? a.nblocks - tile_base : ntiles);
   if constexpr (OG == 2)
-    hipLaunchKernelGGL(F16 ? igemm8_og2_f16_kernel : igemm8_og2_kernel, dim3(a.nblocks, splits), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(F16 ? igemm8_og2_f16_kernel : igemm8_og2_kernel, dim3(grid, splits), dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL(F16 ? igemm8_og1_f16_kernel : igemm8_og1_kernel, dim3(a.nblocks, splits), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(F16 ? igemm8_og1_f16_kernel : igemm8_og1_kernel, dim3(grid, splits), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1100,6 +1106,7 @@ static bool hg4_eligible(int dtype, int cin_p, int cout_p, int kh, int kw, int64
 // split-K.
 struct IgPlan {
   int tile, bo, bp, splits;
+  int tail = 0;  // tile 6, one full-K launch of whole rounds + the remaining tiles split over K in two (see ig_plan)
 };
 
 static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int kw, int64_t x_elems, bool x8 = true) {
@@ -1152,6 +1159,15 @@ static IgPlan ig_plan(int dtype, int64_t M, int cout_p, int cin_p, int kh, int k
     if (g8_split > 1) return IgPlan{tile, BOs[tile], BPs[tile], g8_split};
   }
   IgPlan pl{tile, BOs[tile], BPs[tile], 1};
+  // Wave balance of a full-K 256 x 256 grid (one workgroup per CU on 256 CUs): a last round of r <= 128 tiles runs as
+  // 2r half-K workgroups -- one round of half the time -- behind a launch of the whole rounds; the tail's f32 partials
+  // are combined over its pixels only (SG3-T-256 L0-L2 at batch 32: 362 tiles = 256 + 106, 2 rounds -> 1.5).  Round 6
+  // split every tile of such a grid instead (724 half-K workgroups: 10 % slower, every tile paying the partials).
+  static const bool g8_tail = knob("IC2_G8_TAIL", 1) != 0;
+  if (tile == 6 && g8_tail && splitk && K / 64 >= 16 && M * cout_p < (1LL << 31)) {
+    const int64_t tiles_o = (cout_p + 255) / 256, tiles = ceil_div(M, 256) * tiles_o, rem = tiles % 256;
+    if (tiles > 256 && rem > 0 && rem <= 128 && (tiles - rem) % tiles_o == 0) pl.tail = 1;
+  }
   if (tile < 6 && splitk) {
     // fewer workgroups than ~1.25 per CU: split K so the launch reaches ~512 workgroups, each slice
     // keeping >= 8 chunks of 32
@@ -1508,10 +1524,23 @@ static void launch_torgb(const IgemmArgs& a, hipStream_t s) {
 }
 
 // the 2-byte (bf16 / f16) implicit-GEMM tiles and the halo conv configurations, by operand type
+// first tile of the split tail of a 256 x 256 8-phase grid (IgPlan::tail): the whole rounds before it
+static int g8_tail_first(int64_t M, int cout_p) {
+  const int64_t g6 = ceil_div(M, 256) * ((cout_p + 255) / 256);
+  return (int)(g6 - g6 % 256);
+}
 template <bool F16>
 static void launch_igemm16(const IgemmArgs& a, hipStream_t s, const IgPlan& pl, bool split384, int cout_p) {
   switch (pl.tile) {
-    case 6: launch_g8<2, F16>(a, s, 0, -1, pl.splits); break;
+    case 6:
+      if (pl.tail) {  // whole rounds at full K, then the tail tiles split over K in two (ig_plan)
+        const int full = g8_tail_first(a.M, a.cout_p);
+        launch_g8<2, F16>(a, s, 0, -1, 1, 0, full);
+        launch_g8<2, F16>(a, s, 0, -1, 2, full, -1);
+      } else {
+        launch_g8<2, F16>(a, s, 0, -1, pl.splits);
+      }
+      break;
     case 7:
       if (split384) {
         launch_g8<2, F16>(a, s, 0, cout_p - 128, pl.splits);
@@ -1614,7 +1643,7 @@ static const char* conv_choice_name(const ConvChoice& c, int dtype, int n, int h
     snprintf(buf, sizeof(buf), "igemm_f32_128x128%s", c.pl.splits > 1 ? "_splitk" : "");
     return buf;
   }
-  if (c.pl.tile == 6) return c.pl.splits > 1 ? "igemm8_og2_splitk" : "igemm8_og2";
+  if (c.pl.tile == 6) return c.pl.splits > 1 ? "igemm8_og2_splitk" : c.pl.tail ? "igemm8_og2_tail" : "igemm8_og2";
   if (c.pl.tile == 7) return c.split384 ? "igemm8_og2+og1" : "igemm8_og1";
   snprintf(buf, sizeof(buf), "igemm_%dx%d%s", c.pl.bo, c.pl.bp, c.pl.splits > 1 ? "_splitk" : "");
   return buf;
@@ -1654,7 +1683,8 @@ extern "C" int64_t ic2_conv_igemm_ws_bytes(int dtype, int n, int h, int w_, int 
   if (n <= 0 || h <= 0 || w_ <= 0 || ho <= 0 || wo <= 0 || cin_p <= 0 || cout_p <= 0 || kh <= 0 || kw <= 0) return 0;
   const int nc = conv_chunk_n(dtype, n, h, w_, cin_p);
   const ConvChoice c = conv_choice(dtype, IC2_LAYOUT_NHWC, dtype, nc, h, w_, cin_p, cout_p, cout_p, kh, kw, pad);
-  return c.kind == CK_IGEMM && c.pl.splits > 1 ? (int64_t)c.pl.splits * nc * ho * wo * cout_p * 4 : 0;
+  if (c.kind != CK_IGEMM || (c.pl.splits == 1 && !c.pl.tail)) return 0;
+  return (int64_t)(c.pl.tail ? 2 : c.pl.splits) * nc * ho * wo * cout_p * 4;
 }
 
 extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtype, int out_dtype, int n, int h, int w_,
@@ -1728,6 +1758,7 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
   dtype = kdt;
   IgPlan& pl = c.pl;
   if (pl.splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)pl.splits * M * cout_p * 4)) pl.splits = 1;
+  if (pl.tail && (workspace == nullptr || ws_bytes < 2 * M * cout_p * 4 || a.group != 1)) pl.tail = 0;
   switch (c.kind) {
     case CK_TORGB:
       if (dtype == IC2_F16) launch_torgb<true>(a, s);
@@ -1742,10 +1773,12 @@ extern "C" int ic2_conv_igemm_ws(const void* x, const void* w, void* y, int dtyp
       if (dtype == IC2_F32) launch_igemm<false, 128, 128, 2, 2, 2>(a, pl.splits, s);
       else if (dtype == IC2_F16) launch_igemm16<true>(a, s, pl, c.split384, cout_p);
       else launch_igemm16<false>(a, s, pl, c.split384, cout_p);
-      if (pl.splits > 1) {
-        const int64_t total = M * (cout_p / 4);
+      if (pl.splits > 1 || pl.tail) {
+        // the tail's pixels: its first tile's p-tile (tiles are p-tile major at group 1) times 256
+        const int p_lo = pl.tail ? g8_tail_first(M, cout_p) / ((cout_p + 255) / 256) * 256 : 0;
+        const int64_t total = (M - p_lo) * (cout_p / 4);
         const int grid = (int)(ceil_div(total, 256) < 4096 ? ceil_div(total, 256) : 4096);
-        hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.splits);
+        hipLaunchKernelGGL(igemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, a, pl.tail ? 2 : pl.splits, p_lo);
       }
       break;
   }

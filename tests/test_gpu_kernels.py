@@ -444,6 +444,17 @@ def test_conv_g8_splitk(cuda, cin, cout, size, pad, n, dtype):
     _conv_case(cin, cout, size, pad, dtype, n=n)
 
 
+@pytest.mark.parametrize("cin,cout", [(128, 512), (128, 300)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_g8_tail_split(cuda, cin, cout, dtype):
+    """A full-K 256 x 256 grid of 1.41 rounds (362 tiles at 12 x 62^2 x 512 outputs, the SG3-T-256 L0-L2 shape at
+    batch 32) runs as 256 full-K tiles + the 106 tail tiles split over K in two, the tail's partials combined over its
+    pixels only (tile_base, p_lo): the plan picks it and the result matches F.conv2d in fp64 (partial o-tile: 300)."""
+    dc = nv.F16 if dtype == torch.float16 else nv.BF16
+    assert nv.conv_plan(dc, dc, nv.NHWC, 12, 62, 62, cin, nv.pad32(cout), cout, 3, 3, 1).startswith("igemm8_og2_tail")
+    _conv_case(cin, cout, 62, 1, dtype, n=12)
+
+
 @pytest.mark.parametrize("cin,cout,size,pad", [(128, 362, 88, 2), (96, 384, 81, 1)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_split_384(cuda, cin, cout, size, pad, dtype):

@@ -249,6 +249,11 @@ def test_conv_launch_plan_names():
     # encoder block 0 conv2 in bf16 (64 -> 64 at 256^2): the halo direct conv; split-bf16 (192 tripled channels): hg4
     assert plan(nv.BF16, nv.BF16, nv.NHWC, B, 256, 256, 64, 64, 64, 3, 3, 1) == "hconv_64_64"
     assert plan(nv.BF16, nv.F32, nv.NHWC, B, 256, 256, 192, 64, 64, 3, 3, 1).startswith("hg4_o64")
+    # L0-L2 (512 -> 512, 36^2 pad 2 at batch 32: 362 tiles = 1.41 rounds): whole rounds at full K + the tail split
+    # over K (f32 partials in a caller-owned workspace of 2 x M x cout_p floats); L3 (52^2: 730 tiles) is not split
+    assert plan(nv.F16, nv.F16, nv.NHWC16, B, 36, 36, 512, 512, 512, 3, 3, 2) == "igemm8_og2_tail_f16"
+    assert nv.query("ic2_conv_igemm_ws_bytes", nv.F16, B, 36, 36, 512, 512, 3, 3, 2) == 2 * B * 38 * 38 * 512 * 4
+    assert plan(nv.F16, nv.F16, nv.NHWC16, B, 52, 52, 512, 512, 512, 3, 3, 2) == "igemm8_og2_f16"
     # small late encoder blocks: split-K implicit GEMM; fp32 mode: the exact-f32 tile
     assert plan(nv.BF16, nv.F32, nv.NHWC, B, 4, 4, 1536, 512, 512, 3, 3, 1).endswith("_splitk")
     assert plan(nv.F32, nv.F32, nv.NHWC, 2, 16, 16, 64, 64, 64, 3, 3, 1).startswith("igemm_f32")
